@@ -1,0 +1,170 @@
+/*
+ * trpo_engine.h — C-ABI of the MI355X-native TRPO policy-update engine.
+ *
+ * The reference (inksci/TRPO) runs its update through a TF-1.3 session and
+ * numpy; every entry point below replaces one reference interface, cited as
+ * file:line into the reference tree.  Conventions:
+ *
+ *   - return 0 on success, a negative code on failure; trpo_last_error()
+ *     returns the message of the calling thread's last failure;
+ *   - `mem` selects where a caller pointer lives: TRPO_MEM_HOST or
+ *     TRPO_MEM_DEVICE (a device pointer on the engine's GPU, e.g. a torch-ROCm
+ *     tensor's data_ptr()).  Inputs are copied; caller buffers are never
+ *     retained (reference: caller-owned numpy in, fresh numpy out);
+ *   - one engine is driven from one host thread; calls are ordered on the
+ *     engine's HIP stream and synchronise only when they return host data;
+ *   - flat parameter vectors use the reference's layout
+ *     [W1, b1, W2, b2, ..., WL, bL], W_l row-major [fan_in][fan_out]
+ *     (tf.trainable_variables() order, trpo_inksci.py:49; var_shape/numel,
+ *     utils.py:108-116).
+ *
+ * All arithmetic that the reference does in float32 is float32 here; the
+ * scalars its NumPy-1.x promotion keeps in float64 (shs, lm, the
+ * expected-improve rate, the line-search ratio) are float64.
+ */
+#ifndef TRPO_ENGINE_H
+#define TRPO_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRPO_MEM_HOST 0
+#define TRPO_MEM_DEVICE 1
+
+#define TRPO_OK 0
+#define TRPO_ERR_ARG (-1)
+#define TRPO_ERR_HIP (-2)
+#define TRPO_ERR_RCCL (-3)
+#define TRPO_ERR_STATE (-4)
+
+typedef struct trpo_engine trpo_engine;
+
+/* Hyper-parameters of one update; defaults are config/eps of trpo_inksci.py:16-17
+ * and the CG/line-search defaults of utils.py:171-172,185. */
+typedef struct trpo_update_params {
+  int cg_iters;            /* 10          utils.py:185 */
+  float residual_tol;      /* 1e-10       utils.py:185 (absolute, on r.r) */
+  float cg_damping;        /* 0.1         trpo_inksci.py:17,126 */
+  double max_kl;           /* 0.01        trpo_inksci.py:17,149,157 */
+  int compute_advantages;  /* 1: discount + standardise the rewards given to trpo_set_rewards first */
+  double gamma;            /* 0.95        trpo_inksci.py:17,104 */
+} trpo_update_params;
+
+typedef struct trpo_update_stats {
+  int cg_iters;            /* CG iterations run (early exit on r.r < residual_tol) */
+  int k;                   /* accepted backtrack index (step fraction 0.5^k), -1 if none */
+  int reverted;            /* 1 if kl > 2 max_kl restored theta_prev (trpo_inksci.py:157-158) */
+  int pad;
+  double shs, lm, rate;    /* trpo_inksci.py:148-153 */
+  float surr_before, kl_before, ent_before;   /* losses at theta_prev */
+  float surr_after, kl_after, ent_after;      /* losses at the line-search result (:156) */
+  float rdotr;             /* final CG residual r.r */
+  float gdotstepdir;       /* g . stepdir */
+} trpo_update_stats;
+
+/* Vectors of the last update, for trpo_get_vector(). */
+#define TRPO_VEC_THETA 0       /* current parameters (GetFlat) */
+#define TRPO_VEC_THETA_PREV 1  /* thprev, trpo_inksci.py:144 */
+#define TRPO_VEC_G 2           /* policy gradient, :146 */
+#define TRPO_VEC_STEPDIR 3     /* CG solution, :147 */
+#define TRPO_VEC_FULLSTEP 4    /* :150 */
+#define TRPO_VEC_THETA_LS 5    /* linesearch result before the revert check, :153 */
+
+/* ---- lifecycle --------------------------------------------------------- */
+
+/* Build an engine for the categorical tanh-MLP policy of trpo_inksci.py:38-40
+ * (hidden widths as a list; the reference is the depth-1 case {64}) with room
+ * for `max_rows` states on GPU `device`.  n_actions <= 32. */
+int trpo_create(trpo_engine** out, int obs_dim, const int* hidden, int n_hidden, int n_actions,
+                int64_t max_rows, int device);
+void trpo_destroy(trpo_engine* e);
+const char* trpo_last_error(void);
+int64_t trpo_num_params(const trpo_engine* e);
+int trpo_synchronize(trpo_engine* e);
+/* the engine's HIP stream (hipStream_t) as an opaque pointer */
+void* trpo_stream(trpo_engine* e);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------
+ * The reference is single-process (trpo_inksci.py:23).  Rank 0 creates an id,
+ * the launcher broadcasts it, every rank calls trpo_comm_init.  After that the
+ * FVP / gradient / loss sums of each rank's shard are all-reduced. */
+int trpo_comm_unique_id(uint8_t out_id[128]);
+int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world);
+
+/* ---- parameters: SetFromFlat / GetFlat (utils.py:125-158) ---------------- */
+int trpo_set_flat(trpo_engine* e, const float* theta, int mem);
+int trpo_get_flat(trpo_engine* e, float* theta_out, int mem);
+int trpo_get_vector(trpo_engine* e, int which, float* out, int mem);
+
+/* ---- the feed (trpo_inksci.py:119-122) ------------------------------------
+ * states [n][obs_dim] f32, actions [n] int64 in [0, n_actions), advant [n] f32
+ * (may be NULL when trpo_set_rewards + compute_advantages provide it),
+ * old_dist [n][n_actions] f32.  n_global = rows over all ranks (the 1/N of
+ * reduce_mean, trpo_inksci.py:48-51,56). */
+int trpo_set_batch(trpo_engine* e, int64_t n, int64_t n_global, const float* states,
+                   const int64_t* actions, const float* advant, const float* old_dist, int mem);
+/* rewards [n] f64, episode_starts [n] u8 (1 = first step of a path), baseline [n] f64 or NULL.
+ * The paths of trpo_inksci.py:102-112, concatenated; this rank's shard must begin at a path start. */
+int trpo_set_rewards(trpo_engine* e, const double* rewards, const uint8_t* episode_starts,
+                     const double* baseline, int mem);
+/* returns = discount(rewards, gamma) per path; advant = returns - baseline,
+ * standardised (trpo_inksci.py:102-117).  Optional host copies (f64). */
+int trpo_compute_advantages(trpo_engine* e, double gamma, double* returns_out, double* advant_out,
+                            int mem);
+
+/* ---- the graph outputs ---------------------------------------------------- */
+/* session.run(self.losses) -> [surr, kl, ent] at the current parameters (trpo_inksci.py:53,156) */
+int trpo_losses(trpo_engine* e, float out3[3]);
+/* loss(th): SetFromFlat(th) then session.run(surr) (trpo_inksci.py:127-129); out3 = [surr, kl, ent] */
+int trpo_eval_losses(trpo_engine* e, const float* theta, float out3[3], int mem);
+/* session.run(self.pg) = flatgrad(surr, var_list) (trpo_inksci.py:54,146) */
+int trpo_policy_grad(trpo_engine* e, float* g_out, int mem);
+/* fisher_vector_product(p) = session.run(self.fvp) + cg_damping * p (trpo_inksci.py:56-70,124-126) */
+int trpo_fvp(trpo_engine* e, const float* v, float* out, float damping, int mem);
+
+/* ---- the numpy half --------------------------------------------------------- */
+/* conjugate_gradient(fisher_vector_product, b, cg_iters, residual_tol) (utils.py:185-201),
+ * device-resident: every FVP, dot and axpy stays on the GPU. */
+int trpo_cg(trpo_engine* e, const float* b, float* x_out, int cg_iters, float residual_tol,
+            float damping, int* iters_out, int mem);
+/* conjugate_gradient(f_Ax, b, cg_iters, residual_tol) for an arbitrary host f_Ax
+ * (utils.py:185-201, the reference's generic signature).  The CG vectors, dots and axpys run
+ * on the current GPU in `dtype` (TRPO_F32 / TRPO_F64, the dtype of the caller's b); for each
+ * iteration p is copied out and f_Ax(p, z, ctx) must write z = A p (n elements of dtype) and
+ * return 0.  Engine-free. */
+#define TRPO_F32 0
+#define TRPO_F64 1
+typedef int (*trpo_fax_cb)(const void* p, void* z, void* ctx);
+int trpo_cg_callback(trpo_fax_cb f_Ax, void* ctx, const void* b, void* x_out, int64_t n, int dtype,
+                     int cg_iters, double residual_tol, int* iters_out);
+/* linesearch(loss, x, fullstep, expected_improve_rate) (utils.py:170-182) with f = the policy
+ * surrogate (trpo_inksci.py:127-129).  theta_out = accepted xnew or x; k_out = accepted index or -1.
+ * Leaves the engine's parameters at the last evaluated point, as loss() does. */
+int trpo_linesearch(trpo_engine* e, const float* x, const float* fullstep, double expected_improve_rate,
+                    float* theta_out, int* k_out, int mem);
+
+/* ---- the update block (trpo_inksci.py:101-158) ---------------------------------- */
+void trpo_default_params(trpo_update_params* p);
+int trpo_update(trpo_engine* e, const trpo_update_params* p, trpo_update_stats* stats);
+
+/* ---- engine-free helpers ------------------------------------------------------------ */
+/* number of visible GPUs (0 when none); never fails on a host without GPUs */
+int trpo_device_count(int* out);
+/* discount(x, gamma) (utils.py:14-16) over a concatenation of paths on the current device.
+ * episode_starts may be NULL (one path). */
+int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, double gamma,
+                  double* out, int mem);
+
+/* ---- profiling: per-launch HIP events on the engine stream ------------------------- */
+int trpo_profile_enable(trpo_engine* e, int enable);
+/* JSON {"tag": [count, total_ms], ...}; returns bytes needed (excluding NUL) or < 0 */
+int trpo_profile_query(trpo_engine* e, char* buf, int cap);
+int trpo_profile_reset(trpo_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRPO_ENGINE_H */

@@ -1,0 +1,267 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the golden fixtures and the
+CPU oracle on the same seeded inputs.  Bar: vectors
+norm-relative <= 1e-5 plus elementwise allclose(rtol=1e-5, atol=1e-5 max|b|);
+scalars relative 1e-5; CG iteration count and line-search k exact; integer
+index work exact."""
+import numpy as np
+import pytest
+
+from conftest import assert_vec_close, golden, rel_l2, spec_of, update_fixtures
+from oracle import trpo_oracle as O
+
+pytestmark = pytest.mark.gpu
+REL = 1e-5
+
+
+def make_engine(d, n=None, **kw):
+    from trpo_amd import Engine
+    spec = spec_of(d)
+    n = n or d["X"].shape[0]
+    eng = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=max(n, 16), **kw)
+    eng.set_flat(d["theta"])
+    eng.set_batch(d["X"], d["actions"], np.asarray(d["advant"], np.float32), d["old_dist"])
+    return eng, spec
+
+
+@pytest.mark.parametrize("name", update_fixtures())
+def test_fvp_and_grad_vs_golden(gpu_available, name):
+    d = golden(name)
+    eng, spec = make_engine(d)
+    hv = eng.fvp(d["v"].astype(np.float32), damping=0.0)
+    assert_vec_close(hv, d["hv"], REL, f"{name} Hv")
+    damped = eng.fvp(d["v"].astype(np.float32), damping=0.1)
+    assert_vec_close(damped, d["hv"] + 0.1 * d["v"].astype(np.float32), REL, f"{name} Hv+0.1v")
+    g = eng.policy_grad()
+    assert_vec_close(g, d["g"], REL, f"{name} g")
+    ls = eng.losses()
+    lb = d["losses_before"]
+    # surr and ent are O(1); kl at theta_prev is ~0 in steady state -> absolute bar
+    assert ls[0] == pytest.approx(lb[0], rel=REL, abs=1e-7)
+    assert ls[2] == pytest.approx(lb[2], rel=REL)
+    assert ls[1] == pytest.approx(lb[1], rel=REL, abs=1e-6)
+
+
+def _cg_margin_ok(d, spec):
+    """True when no CG residual lands within 2x of residual_tol (fp32 could flip the exit)."""
+    tol = float(d["residual_tol"])
+    if tol <= 0:
+        return True
+    th = d["theta"].astype(np.float64)
+    b = -d["g"]
+    p, r, rr = b.copy(), b.copy(), b.dot(b)
+    for _ in range(int(d["cg_iters"])):
+        z = O.fisher_vector_product(th, d["X"], p, spec)
+        v = rr / p.dot(z)
+        r = r - v * z
+        new = r.dot(r)
+        p = r + (new / rr) * p
+        rr = new
+        if 0.5 * tol < rr < 2 * tol:
+            return False
+    return True
+
+
+@pytest.mark.parametrize("name", update_fixtures())
+def test_update_vs_golden(gpu_available, name):
+    from trpo_amd import UpdateParams
+    from trpo_amd._lib import VEC_STEPDIR, VEC_FULLSTEP, VEC_THETA_LS, VEC_G
+    d = golden(name)
+    eng, spec = make_engine(d)
+    st = eng.update(UpdateParams(cg_iters=10, residual_tol=float(d["residual_tol"]), max_kl=float(d["max_kl"])))
+    if _cg_margin_ok(d, spec):
+        assert st["cg_iters"] == int(d["cg_iters"])
+        assert_vec_close(eng.get_vector(VEC_STEPDIR), d["stepdir"], REL, f"{name} stepdir")
+        assert st["shs"] == pytest.approx(float(d["shs"]), rel=REL)
+        assert st["lm"] == pytest.approx(float(d["lm"]), rel=REL)
+    assert_vec_close(eng.get_vector(VEC_G), d["g"], REL, f"{name} g")
+    assert st["k"] == int(d["k"])
+    assert bool(st["reverted"]) == bool(d["reverted"])
+    if _cg_margin_ok(d, spec):
+        assert_vec_close(eng.get_vector(VEC_FULLSTEP), d["fullstep"], REL, f"{name} fullstep")
+        assert_vec_close(eng.get_vector(VEC_THETA_LS), d["theta_ls"], REL, f"{name} theta_ls")
+    assert_vec_close(eng.get_flat(), d["theta_new"], REL, f"{name} theta_new")
+    la = d["losses_after"]
+    assert st["surr_after"] == pytest.approx(la[0], rel=REL, abs=1e-7)
+    assert st["kl_after"] == pytest.approx(la[1], rel=REL, abs=1e-7)
+    assert st["ent_after"] == pytest.approx(la[2], rel=REL)
+
+
+@pytest.mark.parametrize("name", ["update_c2.npz", "update_c3.npz", "update_deep_odd.npz"])
+def test_update_forced_iters_vs_oracle(gpu_available, name):
+    """residual_tol = 0 (benchmark mode, exactly 10 CG iterations) vs the oracle run live."""
+    from trpo_amd import UpdateParams
+    from trpo_amd._lib import VEC_STEPDIR
+    d = golden(name)
+    eng, spec = make_engine(d)
+    st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+    r = O.trpo_update(d["theta"].astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], d["old_dist"]),
+                      spec, np.float64, 10, 0.0)
+    assert st["cg_iters"] == 10 == r.cg_iters
+    assert st["k"] == r.k
+    assert_vec_close(eng.get_vector(VEC_STEPDIR), r.stepdir, REL, "stepdir")
+    assert st["shs"] == pytest.approx(r.shs, rel=REL)
+    assert_vec_close(eng.get_flat(), r.theta_new, REL, "theta_new")
+
+
+def test_stepwise_utils_surface_matches_fused(gpu_available):
+    """trpo_inksci.py:144-158 written over trpo_amd.utils == the fused trpo_update."""
+    from trpo_amd import TRPOAgent
+    d = golden("update_c2.npz")
+    spec = spec_of(d)
+    batch = {"state": d["X"], "action": d["actions"], "action_dist": d["old_dist"],
+             "advant": np.asarray(d["advant"], np.float32)}
+    a1 = TRPOAgent(spec.obs_dim, spec.n_actions, spec.hidden, max_rows=4096, theta=d["theta"])
+    a2 = TRPOAgent(spec.obs_dim, spec.n_actions, spec.hidden, max_rows=4096, theta=d["theta"])
+    s1 = a1.update(batch)
+    s2 = a2.update_stepwise(batch)
+    assert_vec_close(a2.gf(), d["theta_new"], REL, "stepwise theta_new")
+    assert_vec_close(a1.gf(), a2.gf(), REL, "fused vs stepwise")
+    assert s2["kl_after"] == pytest.approx(s1["kl_after"], rel=REL)
+
+
+def test_advantages_from_rewards(gpu_available):
+    d = golden("update_c3.npz")
+    eng, spec = make_engine(d)
+    eng.set_rewards(d["rewards"], d["starts"])
+    ret, adv = eng.compute_advantages(0.95)
+    np.testing.assert_allclose(ret, d["returns"], rtol=1e-13)
+    np.testing.assert_allclose(adv, d["advant"], rtol=1e-11, atol=1e-12)
+    # the update that starts from rewards equals the one fed the advantages
+    from trpo_amd import UpdateParams
+    st = eng.update(UpdateParams(compute_advantages=True, gamma=0.95))
+    assert st["k"] == int(d["k"])
+    assert_vec_close(eng.get_flat(), d["theta_new"], REL, "theta_new from rewards")
+
+
+def test_discount_vs_golden(gpu_available):
+    from trpo_amd import utils
+    d = golden("discount.npz")
+    for k in sorted(x[:-2] for x in d.files if x.endswith("_x")):
+        gamma = float(k.split("_")[0][1:])
+        np.testing.assert_allclose(utils.discount(d[k + "_x"], gamma), d[k + "_y"], rtol=1e-13, err_msg=k)
+
+
+@pytest.mark.parametrize("n,p_start", [(1, 0.0), (2, 1.0), (4097, 0.0), (100_003, 0.005),
+                                       (1_000_000, 0.0), (2_000_000, 1.0 / 200)])
+def test_discount_segmented_large(gpu_available, n, p_start):
+    """Sizes past one scan tile / one block-map pass; checked against scipy's lfilter per path."""
+    import scipy.signal
+    from trpo_amd.engine import discount_device
+    rng = np.random.RandomState(n)
+    x = rng.uniform(0, 1, n)
+    starts = (rng.uniform(size=n) < p_start).astype(np.uint8)
+    starts[0] = 1
+    y = discount_device(x, 0.99, starts)
+    idx = list(np.flatnonzero(starts)) + [n]
+    ref = np.empty(n)
+    for a, b in zip(idx[:-1], idx[1:]):
+        ref[a:b] = scipy.signal.lfilter([1], [1, -0.99], x[a:b][::-1])[::-1]
+    np.testing.assert_allclose(y, ref, rtol=1e-12)
+
+
+def test_generic_cg_vs_golden(gpu_available):
+    from trpo_amd import utils
+    d = golden("cg.npz")
+    for case in d["cases"]:
+        base = str(d[case + "_base"])
+        A, b = d[base + "_A"], d[base + "_b"]
+        x, it = utils.conjugate_gradient(lambda p: A @ p, b, int(d[case + "_maxit"]), float(d[case + "_tol"]),
+                                         return_iters=True)
+        assert x.dtype == b.dtype
+        want = d[case + "_x"]
+        if b.dtype == np.float64:
+            assert it == int(d[case + "_iters"]), case
+            assert rel_l2(x, want) < 1e-9, case
+        else:
+            assert abs(it - int(d[case + "_iters"])) <= 1, case
+            assert rel_l2(A.astype(np.float64) @ x, A.astype(np.float64) @ want) < 1e-3 or rel_l2(x, want) < 1e-4, case
+
+
+def test_engine_linesearch_vs_oracle(gpu_available):
+    """linesearch(loss, x, fullstep, rate) on the device vs the oracle, large max_kl
+    fixture (backtracks to k=2) and a rejected search."""
+    from trpo_amd import utils
+    from trpo_amd.utils import EngineLoss
+    d = golden("update_c2_bigkl.npz")
+    eng, spec = make_engine(d)
+    loss = EngineLoss(eng)
+    x = d["theta"].astype(np.float32)
+    full = d["fullstep"].astype(np.float32)
+    res = utils.linesearch(loss, x, full, float(d["rate"]))
+    assert_vec_close(res, d["theta_ls"], REL, "theta_ls")
+    # rejected: a step along +g increases surr -> returns x itself
+    g = d["g"].astype(np.float32)
+    res2 = utils.linesearch(loss, x, g * 10, 1.0)
+    assert res2 is x
+
+
+def test_sharded_partials_sum_to_full(gpu_available):
+    """Two engines on two halves with n_global = N: their partial FVP / grad sum to the full one
+    (what RCCL's all-reduce adds up across ranks)."""
+    from trpo_amd import Engine
+    d = golden("update_c3.npz")
+    spec = spec_of(d)
+    n = d["X"].shape[0]
+    cut = n // 2
+    parts_hv, parts_g = [], []
+    v = d["v"].astype(np.float32)
+    for lo, hi in ((0, cut), (cut, n)):
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+        e.set_flat(d["theta"])
+        e.set_batch(d["X"][lo:hi], d["actions"][lo:hi], np.asarray(d["advant"][lo:hi], np.float32),
+                    d["old_dist"][lo:hi], n_global=n)
+        parts_hv.append(e.fvp(v, 0.0).astype(np.float64))
+        parts_g.append(e.policy_grad().astype(np.float64))
+    assert_vec_close(parts_hv[0] + parts_hv[1], d["hv"], REL, "sharded Hv")
+    assert_vec_close(parts_g[0] + parts_g[1], d["g"], REL, "sharded g")
+
+
+def test_deterministic(gpu_available):
+    d = golden("update_c3.npz")
+    eng, spec = make_engine(d)
+    v = d["v"].astype(np.float32)
+    a = eng.fvp(v, 0.1)
+    b = eng.fvp(v, 0.1)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_large_batch_properties(gpu_available):
+    """At sizes the oracle cannot run quickly: symmetry u.Hv = v.Hu, linearity, and
+    sharding invariance of the FVP; C3 dims, 300k states."""
+    from trpo_amd import Engine
+    spec = O.PolicySpec(128, [64, 64], 18)
+    n = 300_000
+    rng = np.random.RandomState(0)
+    X = rng.standard_normal((n, spec.obs_dim)).astype(np.float32)
+    th = O.init_theta(spec, rng)
+    act = rng.randint(0, spec.n_actions, n)
+    adv = rng.standard_normal(n).astype(np.float32)
+    eng = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+    eng.set_flat(th)
+    # old_dist = p(theta): the engine's own forward via a first batch with uniform old_dist
+    old = np.full((n, spec.n_actions), 1.0 / spec.n_actions, np.float32)
+    eng.set_batch(X, act, adv, old)
+    u = rng.standard_normal(spec.n_params).astype(np.float32)
+    v = rng.standard_normal(spec.n_params).astype(np.float32)
+    Hu = eng.fvp(u, 0.0).astype(np.float64)
+    Hv = eng.fvp(v, 0.0).astype(np.float64)
+    assert abs(u @ Hv - v @ Hu) <= 1e-5 * abs(u @ Hv)
+    Hw = eng.fvp((2.0 * u - 3.0 * v).astype(np.float32), 0.0).astype(np.float64)
+    assert rel_l2(Hw, 2.0 * Hu - 3.0 * Hv) < 1e-5
+    assert u @ Hu > 0 and v @ Hv > 0          # KL Hessian is PSD
+    # a slice checked directly against the oracle
+    m = 3000
+    ref = O.fvp_undamped(th.astype(np.float64), X[:m], u.astype(np.float64), spec, n_global=n)
+    e2 = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=m)
+    e2.set_flat(th)
+    e2.set_batch(X[:m], act[:m], adv[:m], old[:m], n_global=n)
+    assert_vec_close(e2.fvp(u, 0.0), ref, REL, "slice Hv")
+
+
+def test_bad_actions_fail_loudly(gpu_available):
+    from trpo_amd import Engine
+    from trpo_amd._lib import EngineError
+    e = Engine(4, [8], 2, max_rows=8)
+    with pytest.raises(EngineError, match="action"):
+        e.set_batch(np.zeros((4, 4), np.float32), np.array([0, 1, 2, 0]), np.zeros(4, np.float32),
+                    np.full((4, 2), .5, np.float32))

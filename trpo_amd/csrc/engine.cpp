@@ -1,0 +1,1097 @@
+// Runtime of the TRPO update engine behind the C-ABI of include/trpo_engine.h.
+//
+// One engine = one GPU = one shard of the state batch.  It owns every device
+// buffer of the update (HBM layout in DESIGN.md), one HIP stream, and an
+// optional RCCL communicator.  The reference's session.run calls
+// (trpo_inksci.py:126,129,146,156) become kernel sequences on that stream:
+//
+//   prepare()      policy forward at theta + the KL_ff plain backward; caches
+//                  H_l, P, D_l, E_l (fixed while theta is fixed, i.e. over the
+//                  whole CG solve — the reference recomputes them per call)
+//   policy_grad()  surr backward + weight-gradient GEMMs (flatgrad, :54)
+//   fvp()          R-forward + R-backward + weight gradients (:56-70)
+//   cg()           utils.py:185-201 with scalars on device and an early-exit flag
+//   update()       trpo_inksci.py:144-158
+#include "../../include/trpo_engine.h"
+#include "common.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace trpo;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct ArgError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct RcclError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHECK(x)                                                                       \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw HipError(std::string(#x) + " failed: " + hipGetErrorString(e_));              \
+  } while (0)
+#define NCCLCHECK(x)                                                                      \
+  do {                                                                                    \
+    ncclResult_t r_ = (x);                                                                \
+    if (r_ != ncclSuccess) throw RcclError(std::string(#x) + " failed: " + ncclGetErrorString(r_)); \
+  } while (0)
+#define REQUIRE(c, msg)                  \
+  do {                                   \
+    if (!(c)) throw ArgError(msg);       \
+  } while (0)
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return TRPO_OK;
+  } catch (const ArgError& e) {
+    g_last_error = e.what();
+    return TRPO_ERR_ARG;
+  } catch (const RcclError& e) {
+    g_last_error = e.what();
+    return TRPO_ERR_RCCL;
+  } catch (const HipError& e) {
+    g_last_error = e.what();
+    return TRPO_ERR_HIP;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TRPO_ERR_STATE;
+  }
+}
+
+inline int pad4(int x) { return (x + 3) & ~3; }
+
+inline void check_launch() { HIPCHECK(hipGetLastError()); }
+
+}  // namespace
+
+struct trpo_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // policy shape
+  int L = 0;                       // layers
+  std::vector<int> w, wp;          // widths [obs, hidden..., A] and padded
+  int64_t P = 0;
+  std::vector<int64_t> offW, offb;
+  int64_t cap = 0, n = 0, n_global = 0;
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+
+  // ---- device buffers ----
+  std::vector<void*> allocs;
+  float *theta = nullptr, *theta_prev = nullptr, *theta_trial = nullptr, *theta_ls = nullptr;
+  float *g = nullptr, *bneg = nullptr, *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr;
+  float *hv = nullptr, *stepdir = nullptr, *fullstep = nullptr, *vin = nullptr, *vout = nullptr;
+  std::vector<float*> WF, WB, WFt;   // packed [W;V], [W^T;V^T], trial forward weights
+  float* WBt_scratch = nullptr;
+  float* X = nullptr;
+  int* act = nullptr;
+  float *adv32 = nullptr, *old = nullptr;
+  double *rewards = nullptr, *returns = nullptr, *adv64 = nullptr, *baseline = nullptr;
+  uint8_t* starts = nullptr;
+  bool have_baseline = false, have_rewards = false;
+  std::vector<float*> H, D, E, RH, RD;   // indexed as in DESIGN.md
+  float *Pm = nullptr, *DSL = nullptr;
+  double* rowterms = nullptr;
+  float* slab = nullptr;
+  int S = 1, rows_per_split = 16;
+  int64_t slab_stride = 0;
+  double *partA = nullptr, *partB = nullptr, *part3 = nullptr, *local3 = nullptr, *dscal = nullptr;
+  void* scan_ws = nullptr;
+  UpdScalars* sc = nullptr;
+  CGFlags* fl = nullptr;
+  int* dbad = nullptr;
+  UpdScalars* hsc = nullptr;   // pinned host mirror
+
+  bool prepared = false;
+
+  // profiling
+  bool prof = false;
+  struct Ev {
+    std::string tag;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> ev_live;
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, std::pair<long, double>> prof_acc;
+
+  // ------------------------------------------------------------------------
+  template <class T>
+  T* dalloc(size_t count) {
+    void* ptr = nullptr;
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    HIPCHECK(hipMalloc(&ptr, bytes));
+    HIPCHECK(hipMemsetAsync(ptr, 0, bytes, stream));
+    allocs.push_back(ptr);
+    return static_cast<T*>(ptr);
+  }
+
+  void use() { HIPCHECK(hipSetDevice(device)); }
+
+  const float* act_in(int l) const { return l == 0 ? X : H[l]; }
+
+  hipEvent_t take_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e));
+    return e;
+  }
+  struct Scope {
+    trpo_engine* e;
+    int idx = -1;
+    Scope(trpo_engine* eng, const char* tag) : e(eng) {
+      if (!e->prof) return;
+      Ev ev{tag, e->take_event(), e->take_event()};
+      HIPCHECK(hipEventRecord(ev.a, e->stream));
+      e->ev_live.push_back(ev);
+      idx = (int)e->ev_live.size() - 1;
+    }
+    ~Scope() {
+      if (idx >= 0) (void)hipEventRecord(e->ev_live[idx].b, e->stream);
+    }
+  };
+  void prof_collect() {
+    if (ev_live.empty()) return;
+    HIPCHECK(hipStreamSynchronize(stream));
+    for (auto& ev : ev_live) {
+      float ms = 0.f;
+      HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
+      auto& acc = prof_acc[ev.tag];
+      acc.first += 1;
+      acc.second += ms;
+      ev_pool.push_back(ev.a);
+      ev_pool.push_back(ev.b);
+    }
+    ev_live.clear();
+  }
+
+  // ------------------------------------------------------------------------
+  void init(int obs, const int* hidden, int nh, int A, int64_t max_rows, int dev) {
+    REQUIRE(obs > 0 && A > 0 && nh >= 0 && max_rows > 0, "invalid policy dimensions");
+    REQUIRE(nh + 1 <= kMaxLayers, "too many layers");
+    REQUIRE(A <= 32, "n_actions must be <= 32 (one wave-half softmax row)");
+    REQUIRE(max_rows < (int64_t(1) << 31), "max_rows must fit in int32 row indices");
+    device = dev;
+    use();
+    HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    w.push_back(obs);
+    for (int i = 0; i < nh; ++i) {
+      REQUIRE(hidden[i] > 0, "hidden widths must be positive");
+      w.push_back(hidden[i]);
+    }
+    w.push_back(A);
+    L = (int)w.size() - 1;
+    for (int v : w) wp.push_back(pad4(v));
+    P = 0;
+    for (int l = 0; l < L; ++l) {
+      offW.push_back(P);
+      P += (int64_t)w[l] * w[l + 1];
+      offb.push_back(P);
+      P += w[l + 1];
+    }
+    cap = max_rows;
+
+    for (float** v : {&theta, &theta_prev, &theta_trial, &theta_ls, &g, &bneg, &x, &r, &p, &z, &hv,
+                      &stepdir, &fullstep, &vin, &vout})
+      *v = dalloc<float>(P);
+    int maxpad = 4;
+    for (int l = 0; l < L; ++l) {
+      WF.push_back(dalloc<float>((size_t)2 * wp[l] * wp[l + 1]));
+      WB.push_back(dalloc<float>((size_t)2 * wp[l + 1] * wp[l]));
+      WFt.push_back(dalloc<float>((size_t)2 * wp[l] * wp[l + 1]));
+      maxpad = std::max<int>(maxpad, 2 * wp[l] * wp[l + 1]);
+    }
+    WBt_scratch = dalloc<float>(maxpad);
+    X = dalloc<float>((size_t)cap * wp[0]);
+    act = dalloc<int>(cap);
+    adv32 = dalloc<float>(cap);
+    old = dalloc<float>((size_t)cap * wp[L]);
+    rewards = dalloc<double>(cap);
+    returns = dalloc<double>(cap);
+    adv64 = dalloc<double>(cap);
+    baseline = dalloc<double>(cap);
+    starts = dalloc<uint8_t>(cap);
+    H.assign(L + 1, nullptr);
+    RH.assign(L + 1, nullptr);
+    D.assign(L, nullptr);
+    RD.assign(L, nullptr);
+    E.assign(L, nullptr);
+    for (int l = 1; l < L; ++l) {
+      H[l] = dalloc<float>((size_t)cap * wp[l]);
+      RH[l] = dalloc<float>((size_t)cap * wp[l]);
+    }
+    for (int l = 0; l < L; ++l) {
+      D[l] = dalloc<float>((size_t)cap * wp[l + 1]);
+      RD[l] = dalloc<float>((size_t)cap * wp[l + 1]);
+      if (l < L - 1) E[l] = dalloc<float>((size_t)cap * wp[l + 1]);
+    }
+    Pm = dalloc<float>((size_t)cap * wp[L]);
+    DSL = dalloc<float>((size_t)cap * wp[L]);
+    rowterms = dalloc<double>((size_t)cap * 4);
+    // split-K slabs for the weight gradients
+    int tiles_max = 1;
+    for (int l = 0; l < L; ++l)
+      tiles_max = std::max(tiles_max, ((w[l] + 255) / 256) * ((w[l + 1] + 255) / 256));
+    const int s_target = std::max(1, std::min(512, 1024 / tiles_max));
+    slab_stride = (P + 63) / 64 * 64;
+    slab = dalloc<float>((size_t)s_target * slab_stride);
+    S = s_target;
+    partA = dalloc<double>(kRedBlocks * 3);
+    partB = dalloc<double>(kRedBlocks * 3);
+    part3 = dalloc<double>(kRedBlocks * 3);
+    local3 = dalloc<double>(4);
+    dscal = dalloc<double>(8);
+    scan_ws = dalloc<uint8_t>(discount_workspace_bytes(cap));
+    sc = dalloc<UpdScalars>(1);
+    fl = dalloc<CGFlags>(1);
+    dbad = dalloc<int>(1);
+    HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
+    std::memset(hsc, 0, sizeof(UpdScalars));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  void release() {
+    if (device >= 0) (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& ev : ev_live) {
+      (void)hipEventDestroy(ev.a);
+      (void)hipEventDestroy(ev.b);
+    }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+    for (void* ptr : allocs) (void)hipFree(ptr);
+    allocs.clear();
+    if (hsc) (void)hipHostFree(hsc);
+    if (comm) (void)ncclCommDestroy(comm);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  void set_splits() {
+    // rows per split: a multiple of the 16-row k-tile, >= 64 rows
+    const int smax = S;
+    int64_t rps = (n + smax - 1) / smax;
+    rps = std::max<int64_t>(64, (rps + 15) / 16 * 16);
+    rows_per_split = (int)rps;
+    active_splits = (int)std::max<int64_t>(1, (n + rps - 1) / rps);
+  }
+  int active_splits = 1;
+
+  void copy_in(void* dst, const void* src, size_t bytes, int mem) {
+    if (bytes == 0) return;
+    HIPCHECK(hipMemcpyAsync(dst, src, bytes, mem == TRPO_MEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                     : hipMemcpyHostToDevice,
+                            stream));
+    if (mem != TRPO_MEM_DEVICE) HIPCHECK(hipStreamSynchronize(stream));
+  }
+  void copy_out(void* dst, const void* src, size_t bytes, int mem) {
+    if (bytes == 0) return;
+    HIPCHECK(hipMemcpyAsync(dst, src, bytes, mem == TRPO_MEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                     : hipMemcpyDeviceToHost,
+                            stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  void allreduce_f32(float* buf, size_t count) {
+    if (world <= 1) return;
+    Scope sp(this, "allreduce");
+    NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, stream));
+  }
+  void allreduce_f64(double* buf, size_t count) {
+    if (world <= 1) return;
+    NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream));
+  }
+
+  // ------------------------------------------------------------------------
+  PackArgs pack_args(const std::vector<float*>& wf, const std::vector<float*>* wb) {
+    PackArgs pa{};
+    pa.nl = L;
+    for (int l = 0; l < L; ++l) {
+      pa.L[l].off_w = offW[l];
+      pa.L[l].a = w[l];
+      pa.L[l].b = w[l + 1];
+      pa.L[l].apad = wp[l];
+      pa.L[l].bpad = wp[l + 1];
+      pa.L[l].WF = wf[l];
+      pa.L[l].WB = wb ? (*wb)[l] : nullptr;
+    }
+    return pa;
+  }
+
+  RowGemmArgs row_args(int l_out_width, int l_out_pad) {
+    RowGemmArgs a{};
+    a.M = (int)n;
+    a.N = l_out_width;
+    a.Npad = l_out_pad;
+    return a;
+  }
+
+  // forward through layers 0..L-1 with weights packed in wf (W half); the head
+  // epilogue is `head`; hidden activations go to `hout`
+  void forward(const std::vector<float*>& wf, const float* th, const std::vector<float*>& hout,
+               RowEpi head, const char* tag) {
+    for (int l = 0; l < L; ++l) {
+      RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
+      a.nseg = 1;
+      a.seg[0] = GemmSeg{l == 0 ? X : hout[l], wf[l], wp[l], wp[l + 1], wp[l]};
+      a.ea.bias = th + offb[l];
+      a.ea.ldo = wp[l + 1];
+      if (l < L - 1) {
+        a.epi = RowEpi::kTanh;
+        a.ea.out0 = hout[l + 1];
+      } else {
+        a.epi = head;
+        a.ea.out0 = Pm;
+        a.ea.out1 = D[L - 1];
+        a.ea.out2 = DSL;
+        a.ea.old = old;
+        a.ea.act = act;
+        a.ea.adv = adv32;
+        a.ea.rowterms = rowterms;
+        a.ea.invN = 1.0 / (double)n_global;
+      }
+      Scope sp(this, tag);
+      launch_rowgemm(a, stream);
+      check_launch();
+    }
+  }
+
+  // rowterms -> [surr, kl, ent] into sc->loss_before (which=0) or loss_trial (which=1)
+  void reduce_losses(int which, const int* skip) {
+    launch_rowterms_partials(rowterms, n, part3, skip, stream);
+    launch_rowterms_finish(part3, local3, skip, stream);
+    allreduce_f64(local3, 3);
+    launch_losses_store(local3, 1.0 / (double)n_global, sc, which, skip, stream);
+    check_launch();
+  }
+
+  void require_batch() { REQUIRE(n > 0, "no batch: call trpo_set_batch first"); }
+
+  // policy forward + KL_ff plain backward at theta (cached over CG)
+  void prepare() {
+    require_batch();
+    if (prepared) return;
+    PackArgs pa = pack_args(WF, &WB);
+    launch_pack(pa, theta, 0, nullptr, stream);
+    forward(WF, theta, H, RowEpi::kPrepHead, "fwd");
+    // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H
+    for (int l = L - 1; l >= 1; --l) {
+      RowGemmArgs a = row_args(w[l], wp[l]);
+      a.nseg = 1;
+      a.seg[0] = GemmSeg{D[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+      a.epi = RowEpi::kPrepBwd;
+      a.ea.H = H[l];
+      a.ea.out0 = D[l - 1];
+      a.ea.out1 = E[l - 1];
+      a.ea.ldo = wp[l];
+      Scope sp(this, "bwd");
+      launch_rowgemm(a, stream);
+      check_launch();
+    }
+    reduce_losses(0, nullptr);
+    prepared = true;
+  }
+
+  // sum over splits -> out (local partial) ; all-reduce
+  void reduce_grad(float* out, const int* skip) {
+    {
+      Scope sp(this, "reduce");
+      launch_reduce_slab(slab, active_splits, slab_stride, P, out, skip, stream);
+      check_launch();
+    }
+    allreduce_f32(out, (size_t)P);
+  }
+
+  void wgrad_layer(int l, int nseg, WSeg s0, WSeg s1, int colsum_seg, const int* skip, const char* tag) {
+    WGradArgs a{};
+    a.rows = (int)n;
+    a.Ma = w[l];
+    a.Nb = w[l + 1];
+    a.Mpad = wp[l];
+    a.Npad = wp[l + 1];
+    a.nseg = nseg;
+    a.seg[0] = s0;
+    a.seg[1] = s1;
+    a.colsum_seg = colsum_seg;
+    a.splits = active_splits;
+    a.rows_per_split = rows_per_split;
+    a.slab = slab;
+    a.slab_stride = slab_stride;
+    a.off_w = offW[l];
+    a.off_b = offb[l];
+    a.skip = skip;
+    Scope sp(this, tag);
+    launch_wgrad(a, stream);
+    check_launch();
+  }
+
+  // flatgrad(surr) (trpo_inksci.py:54) -> g (all ranks)
+  void policy_grad() {
+    prepare();
+    // surr backward: DS_{l-1} = (DS_l W_l^T)(1-H_l^2) ; DS of hidden layers lives in RD scratch
+    std::vector<float*> DS(L);
+    DS[L - 1] = DSL;
+    for (int l = 0; l < L - 1; ++l) DS[l] = RD[l];
+    for (int l = L - 1; l >= 1; --l) {
+      RowGemmArgs a = row_args(w[l], wp[l]);
+      a.nseg = 1;
+      a.seg[0] = GemmSeg{DS[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+      a.epi = RowEpi::kPgBwd;
+      a.ea.H = H[l];
+      a.ea.out0 = DS[l - 1];
+      a.ea.ldo = wp[l];
+      Scope sp(this, "pg_bwd");
+      launch_rowgemm(a, stream);
+      check_launch();
+    }
+    for (int l = 0; l < L; ++l)
+      wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1]}, WSeg{}, 0, nullptr, "pg_wgrad");
+    reduce_grad(g, nullptr);
+  }
+
+  // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
+  void fvp(const float* v, float* out, const int* skip) {
+    prepare();
+    {
+      PackArgs pa = pack_args(WF, &WB);
+      launch_pack(pa, v, 1, skip, stream);
+      check_launch();
+    }
+    // R-forward
+    for (int l = 0; l < L; ++l) {
+      RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
+      float* Vpart = WF[l] + (size_t)wp[l] * wp[l + 1];
+      if (l == 0) {
+        a.nseg = 1;
+        a.seg[0] = GemmSeg{X, Vpart, wp[0], wp[1], wp[0]};
+      } else {
+        a.nseg = 2;
+        a.seg[0] = GemmSeg{RH[l], WF[l], wp[l], wp[l + 1], wp[l]};
+        a.seg[1] = GemmSeg{H[l], Vpart, wp[l], wp[l + 1], wp[l]};
+      }
+      a.skip = skip;
+      a.ea.bias = v + offb[l];
+      a.ea.ldo = wp[l + 1];
+      if (l < L - 1) {
+        a.epi = RowEpi::kRHidden;
+        a.ea.H = H[l + 1];
+        a.ea.out0 = RH[l + 1];
+      } else {
+        a.epi = RowEpi::kRHead;
+        a.ea.P = Pm;
+        a.ea.out0 = RD[L - 1];
+        a.ea.invN = 1.0 / (double)n_global;
+      }
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_rfwd_l%d", l);
+      Scope sp(this, tag);
+      launch_rowgemm(a, stream);
+      check_launch();
+    }
+    // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
+    for (int l = L - 1; l >= 1; --l) {
+      RowGemmArgs a = row_args(w[l], wp[l]);
+      a.nseg = 2;
+      a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+      a.seg[1] = GemmSeg{D[l], WB[l] + (size_t)wp[l + 1] * wp[l], wp[l + 1], wp[l], wp[l + 1]};
+      a.skip = skip;
+      a.epi = RowEpi::kRBwd;
+      a.ea.H = H[l];
+      a.ea.E = E[l - 1];
+      a.ea.RH = RH[l];
+      a.ea.out0 = RD[l - 1];
+      a.ea.ldo = wp[l];
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_rbwd_l%d", l);
+      Scope sp(this, tag);
+      launch_rowgemm(a, stream);
+      check_launch();
+    }
+    // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
+    for (int l = 0; l < L; ++l) {
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
+      if (l == 0)
+        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1]}, WSeg{}, 0, skip, tag);
+      else
+        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1]}, WSeg{H[l], RD[l], wp[l], wp[l + 1]}, 1,
+                    skip, tag);
+    }
+    reduce_grad(out, skip);
+  }
+
+  // conjugate_gradient(fvp, b) (utils.py:185-201): b, x device vectors
+  void cg(const float* b, float* xo, int iters, float tol, float damping) {
+    REQUIRE(iters >= 0 && iters <= kMaxCG, "cg_iters out of range");
+    prepare();
+    launch_cg_init(b, xo, r, p, P, partA, sc, fl, tol, damping, stream);
+    check_launch();
+    for (int it = 0; it < iters; ++it) {
+      fvp(p, hv, &fl->done[it]);
+      Scope sp(this, "cg_vec");
+      launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      check_launch();
+    }
+  }
+
+  void fetch_scalars() {
+    HIPCHECK(hipMemcpyAsync(hsc, sc, sizeof(UpdScalars), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  // loss(th) at a device parameter vector, without touching the prepared cache
+  void eval_losses_dev(const float* th) {
+    require_batch();
+    PackArgs pa = pack_args(WFt, nullptr);
+    launch_pack(pa, th, 0, nullptr, stream);
+    forward(WFt, th, RH, RowEpi::kLossHead, "ls_fwd");
+    reduce_losses(1, nullptr);
+  }
+
+  void compute_advantages(double gamma) {
+    REQUIRE(have_rewards, "no rewards: call trpo_set_rewards first");
+    launch_discount(rewards, starts, n, gamma, returns, scan_ws, stream);
+    launch_adv_center_partials(returns, have_baseline ? baseline : nullptr, adv64, n, partA, stream);
+    launch_sum_finish(partA, dscal, stream);
+    allreduce_f64(dscal, 1);
+    const double inv_n = 1.0 / (double)n_global;
+    launch_adv_sq_partials(adv64, n, dscal, inv_n, partA, stream);
+    launch_sum_finish(partA, dscal + 1, stream);
+    allreduce_f64(dscal + 1, 1);
+    launch_adv_normalize(adv64, adv32, n, dscal, dscal + 1, inv_n, stream);
+    check_launch();
+    prepared = false;
+  }
+
+  void update(const trpo_update_params& prm, trpo_update_stats* st) {
+    require_batch();
+    REQUIRE(prm.cg_iters >= 0 && prm.cg_iters <= kMaxCG, "cg_iters out of range");
+    if (prm.compute_advantages) {
+      Scope sp(this, "advantages");
+      compute_advantages(prm.gamma);
+    }
+    prepare();
+    // thprev = self.gf()  (:144)
+    HIPCHECK(hipMemcpyAsync(theta_prev, theta, P * sizeof(float), hipMemcpyDeviceToDevice, stream));
+    // g = session.run(pg)  (:146)
+    policy_grad();
+    // stepdir = conjugate_gradient(fisher_vector_product, -g)  (:147)
+    launch_scale_copy(g, bneg, -1.0f, P, stream);
+    cg(bneg, stepdir, prm.cg_iters, prm.residual_tol, prm.cg_damping);
+    // shs = .5 * stepdir.dot(fisher_vector_product(stepdir)) ; lm ; fullstep ; rate  (:148-151)
+    fvp(stepdir, hv, nullptr);
+    {
+      // max_kl goes to the scalar block before shs_finish reads it
+      HIPCHECK(hipMemcpyAsync(&sc->max_kl, &prm.max_kl, sizeof(double), hipMemcpyHostToDevice, stream));
+      Scope sp(this, "step_scale");
+      launch_shs_partials(hv, stepdir, g, P, sc, partA, partB, stream);
+      launch_shs_finish(partA, partB, sc, stream);
+      launch_fullstep(stepdir, fullstep, P, sc, stream);
+      check_launch();
+    }
+    // theta = linesearch(loss, thprev, fullstep, neggdotstepdir / lm)  (:153)
+    for (int k = 0; k < 10; ++k) {
+      launch_ls_trial(theta_prev, fullstep, theta_trial, P, k, sc, stream);
+      eval_losses_dev(theta_trial);
+      launch_ls_decide(sc, k, stream);
+      check_launch();
+      fetch_scalars();
+      if (hsc->accepted) break;
+    }
+    // sff(theta) ; losses ; revert if kl > 2 max_kl  (:154-158)
+    launch_ls_finalize(theta_prev, fullstep, theta, theta_ls, P, sc, stream);
+    check_launch();
+    prepared = false;
+    fetch_scalars();
+    if (st) {
+      st->cg_iters = hsc->iters;
+      st->k = hsc->accepted ? hsc->k : -1;
+      st->reverted = hsc->reverted;
+      st->shs = hsc->shs;
+      st->lm = hsc->lm;
+      st->rate = hsc->rate;
+      st->surr_before = hsc->loss_before[0];
+      st->kl_before = hsc->loss_before[1];
+      st->ent_before = hsc->loss_before[2];
+      st->surr_after = hsc->loss_after[0];
+      st->kl_after = hsc->loss_after[1];
+      st->ent_after = hsc->loss_after[2];
+      st->rdotr = hsc->rdotr[hsc->iters & 1];
+      st->gdotstepdir = hsc->gdots;
+    }
+  }
+};
+
+// =============================================================================
+// C-ABI
+// =============================================================================
+extern "C" {
+
+const char* trpo_last_error(void) { return g_last_error.c_str(); }
+
+int trpo_create(trpo_engine** out, int obs_dim, const int* hidden, int n_hidden, int n_actions,
+                int64_t max_rows, int device) {
+  return guarded([&] {
+    REQUIRE(out, "out is NULL");
+    REQUIRE(n_hidden == 0 || hidden, "hidden is NULL");
+    auto e = std::make_unique<trpo_engine>();
+    try {
+      e->init(obs_dim, hidden, n_hidden, n_actions, max_rows, device);
+    } catch (...) {
+      e->release();
+      throw;
+    }
+    *out = e.release();
+  });
+}
+
+void trpo_destroy(trpo_engine* e) {
+  if (!e) return;
+  e->release();
+  delete e;
+}
+
+int64_t trpo_num_params(const trpo_engine* e) { return e ? e->P : -1; }
+
+int trpo_synchronize(trpo_engine* e) {
+  return guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    HIPCHECK(hipStreamSynchronize(e->stream));
+  });
+}
+
+void* trpo_stream(trpo_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int trpo_comm_unique_id(uint8_t out_id[128]) {
+  return guarded([&] {
+    REQUIRE(out_id, "out_id is NULL");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCLCHECK(ncclGetUniqueId(&id));
+    std::memcpy(out_id, &id, sizeof id);
+  });
+}
+
+int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world) {
+  return guarded([&] {
+    REQUIRE(e && id, "NULL argument");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    e->use();
+    if (e->comm) {
+      NCCLCHECK(ncclCommDestroy(e->comm));
+      e->comm = nullptr;
+    }
+    e->rank = rank;
+    e->world = world;
+    if (world > 1) {
+      ncclUniqueId uid;
+      std::memcpy(&uid, id, sizeof uid);
+      NCCLCHECK(ncclCommInitRank(&e->comm, world, uid, rank));
+    }
+  });
+}
+
+int trpo_set_flat(trpo_engine* e, const float* theta, int mem) {
+  return guarded([&] {
+    REQUIRE(e && theta, "NULL argument");
+    e->use();
+    e->copy_in(e->theta, theta, e->P * sizeof(float), mem);
+    e->prepared = false;
+  });
+}
+
+int trpo_get_flat(trpo_engine* e, float* out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && out, "NULL argument");
+    e->use();
+    e->copy_out(out, e->theta, e->P * sizeof(float), mem);
+  });
+}
+
+int trpo_get_vector(trpo_engine* e, int which, float* out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && out, "NULL argument");
+    e->use();
+    const float* src = nullptr;
+    switch (which) {
+      case TRPO_VEC_THETA: src = e->theta; break;
+      case TRPO_VEC_THETA_PREV: src = e->theta_prev; break;
+      case TRPO_VEC_G: src = e->g; break;
+      case TRPO_VEC_STEPDIR: src = e->stepdir; break;
+      case TRPO_VEC_FULLSTEP: src = e->fullstep; break;
+      case TRPO_VEC_THETA_LS: src = e->theta_ls; break;
+      default: throw ArgError("unknown vector id");
+    }
+    e->copy_out(out, src, e->P * sizeof(float), mem);
+  });
+}
+
+int trpo_set_batch(trpo_engine* e, int64_t n, int64_t n_global, const float* states,
+                   const int64_t* actions, const float* advant, const float* old_dist, int mem) {
+  return guarded([&] {
+    REQUIRE(e && states && actions && old_dist, "NULL argument");
+    REQUIRE(n > 0 && n <= e->cap, "n out of range (0 < n <= max_rows)");
+    REQUIRE(n_global >= n, "n_global must be >= n");
+    e->use();
+    e->n = n;
+    e->n_global = n_global;
+    const int obs = e->w[0], A = e->w[e->L];
+    // states -> [n][pad4(obs)], old_dist -> [n][pad4(A)] (padding zero)
+    auto stage = [&](const float* src, int width, int ldp, float* dst) {
+      if (width == ldp) {
+        e->copy_in(dst, src, (size_t)n * width * sizeof(float), mem);
+        return;
+      }
+      float* tmp = nullptr;
+      HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)n * width * sizeof(float), e->stream));
+      e->copy_in(tmp, src, (size_t)n * width * sizeof(float), mem);
+      launch_copy_rows(tmp, n, width, width, dst, ldp, e->stream);
+      check_launch();
+      HIPCHECK(hipFreeAsync(tmp, e->stream));
+    };
+    stage(states, obs, e->wp[0], e->X);
+    stage(old_dist, A, e->wp[e->L], e->old);
+    int64_t* tmp = nullptr;
+    HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)n * sizeof(int64_t), e->stream));
+    e->copy_in(tmp, actions, (size_t)n * sizeof(int64_t), mem);
+    HIPCHECK(hipMemsetAsync(e->dbad, 0, sizeof(int), e->stream));
+    launch_i64_to_i32(tmp, e->act, n, e->dbad, A, e->stream);
+    check_launch();
+    HIPCHECK(hipFreeAsync(tmp, e->stream));
+    int bad = 0;
+    e->copy_out(&bad, e->dbad, sizeof(int), TRPO_MEM_HOST);
+    REQUIRE(!bad, "action index out of range [0, n_actions)");
+    if (advant) e->copy_in(e->adv32, advant, (size_t)n * sizeof(float), mem);
+    e->set_splits();
+    e->prepared = false;
+    e->have_rewards = false;
+  });
+}
+
+int trpo_set_rewards(trpo_engine* e, const double* rewards, const uint8_t* starts,
+                     const double* baseline, int mem) {
+  return guarded([&] {
+    REQUIRE(e && rewards && starts, "NULL argument");
+    e->require_batch();
+    e->use();
+    e->copy_in(e->rewards, rewards, (size_t)e->n * sizeof(double), mem);
+    e->copy_in(e->starts, starts, (size_t)e->n, mem);
+    e->have_baseline = baseline != nullptr;
+    if (baseline) e->copy_in(e->baseline, baseline, (size_t)e->n * sizeof(double), mem);
+    e->have_rewards = true;
+  });
+}
+
+int trpo_compute_advantages(trpo_engine* e, double gamma, double* returns_out, double* advant_out,
+                            int mem) {
+  return guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    e->compute_advantages(gamma);
+    if (returns_out) e->copy_out(returns_out, e->returns, (size_t)e->n * sizeof(double), mem);
+    if (advant_out) e->copy_out(advant_out, e->adv64, (size_t)e->n * sizeof(double), mem);
+  });
+}
+
+int trpo_losses(trpo_engine* e, float out3[3]) {
+  return guarded([&] {
+    REQUIRE(e && out3, "NULL argument");
+    e->use();
+    e->prepare();
+    e->fetch_scalars();
+    std::memcpy(out3, e->hsc->loss_before, 3 * sizeof(float));
+  });
+}
+
+int trpo_eval_losses(trpo_engine* e, const float* theta, float out3[3], int mem) {
+  return guarded([&] {
+    REQUIRE(e && theta && out3, "NULL argument");
+    e->use();
+    e->copy_in(e->theta, theta, e->P * sizeof(float), mem);   // sff(th), trpo_inksci.py:128
+    e->prepared = false;
+    e->eval_losses_dev(e->theta);
+    e->fetch_scalars();
+    std::memcpy(out3, e->hsc->loss_trial, 3 * sizeof(float));
+  });
+}
+
+int trpo_policy_grad(trpo_engine* e, float* g_out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && g_out, "NULL argument");
+    e->use();
+    e->policy_grad();
+    e->copy_out(g_out, e->g, e->P * sizeof(float), mem);
+  });
+}
+
+int trpo_fvp(trpo_engine* e, const float* v, float* out, float damping, int mem) {
+  return guarded([&] {
+    REQUIRE(e && v && out, "NULL argument");
+    e->use();
+    e->copy_in(e->vin, v, e->P * sizeof(float), mem);
+    e->fvp(e->vin, e->hv, nullptr);
+    // out = fvp + damping * v  (float32, trpo_inksci.py:126)
+    HIPCHECK(hipMemcpyAsync(e->vout, e->hv, e->P * sizeof(float), hipMemcpyDeviceToDevice, e->stream));
+    if (damping != 0.0f) {
+      float* tmp = e->z;
+      launch_scale_copy(e->vin, tmp, damping, e->P, e->stream);
+      launch_axpby(e->vout, tmp, 1.0f, 1.0f, e->P, e->stream);
+      check_launch();
+    }
+    e->copy_out(out, e->vout, e->P * sizeof(float), mem);
+  });
+}
+
+int trpo_cg(trpo_engine* e, const float* b, float* x_out, int cg_iters, float residual_tol,
+            float damping, int* iters_out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && b && x_out, "NULL argument");
+    e->use();
+    e->copy_in(e->bneg, b, e->P * sizeof(float), mem);
+    e->cg(e->bneg, e->stepdir, cg_iters, residual_tol, damping);
+    e->copy_out(x_out, e->stepdir, e->P * sizeof(float), mem);
+    e->fetch_scalars();
+    if (iters_out) *iters_out = e->hsc->iters;
+  });
+}
+
+int trpo_cg_callback(trpo_fax_cb f_Ax, void* ctx, const void* b, void* x_out, int64_t n, int dtype,
+                     int cg_iters, double residual_tol, int* iters_out) {
+  return guarded([&] {
+    REQUIRE(f_Ax && b && x_out, "NULL argument");
+    REQUIRE(n > 0, "n must be positive");
+    REQUIRE(dtype == TRPO_F32 || dtype == TRPO_F64, "dtype must be TRPO_F32 or TRPO_F64");
+    REQUIRE(cg_iters >= 0 && cg_iters <= kMaxCG, "cg_iters out of range");
+    const size_t es = dtype == TRPO_F64 ? 8 : 4;
+    const size_t bytes = (size_t)n * es;
+    hipStream_t s = nullptr;
+    HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void*> bufs;
+    auto alloc = [&](size_t by) {
+      void* p = nullptr;
+      HIPCHECK(hipMalloc(&p, std::max<size_t>(by, 16)));
+      HIPCHECK(hipMemsetAsync(p, 0, std::max<size_t>(by, 16), s));
+      bufs.push_back(p);
+      return p;
+    };
+    try {
+      void *db = alloc(bytes), *dx = alloc(bytes), *dr = alloc(bytes), *dp = alloc(bytes),
+           *dz = alloc(bytes), *dhv = alloc(bytes);
+      double* pa = (double*)alloc(kRedBlocks * sizeof(double));
+      double* pb = (double*)alloc(kRedBlocks * sizeof(double));
+      CGFlags* fl = (CGFlags*)alloc(sizeof(CGFlags));
+      void* sc = alloc(std::max(sizeof(UpdScalars), sizeof(CGScalarsD)));
+      std::vector<uint8_t> ph(bytes), zh(bytes);
+      HIPCHECK(hipMemcpyAsync(db, b, bytes, hipMemcpyHostToDevice, s));
+      if (dtype == TRPO_F64)
+        launch_cg_init_d((double*)db, (double*)dx, (double*)dr, (double*)dp, n, pa, (CGScalarsD*)sc, fl,
+                         residual_tol, s);
+      else
+        launch_cg_init((float*)db, (float*)dx, (float*)dr, (float*)dp, n, pa, (UpdScalars*)sc, fl,
+                       (float)residual_tol, 0.0f, s);
+      HIPCHECK(hipGetLastError());
+      int iters = 0;
+      for (int it = 0; it < cg_iters; ++it) {
+        int done = 0;
+        HIPCHECK(hipMemcpyAsync(&done, &fl->done[it], sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipMemcpyAsync(ph.data(), dp, bytes, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (done) break;
+        REQUIRE(f_Ax(ph.data(), zh.data(), ctx) == 0, "f_Ax callback failed");
+        HIPCHECK(hipMemcpyAsync(dhv, zh.data(), bytes, hipMemcpyHostToDevice, s));
+        if (dtype == TRPO_F64)
+          launch_cg_iter_d((double*)dhv, (double*)dx, (double*)dr, (double*)dp, (double*)dz, n,
+                           (CGScalarsD*)sc, pa, pb, fl, it, s);
+        else
+          launch_cg_iter((float*)dhv, (float*)dx, (float*)dr, (float*)dp, (float*)dz, n, (UpdScalars*)sc,
+                         pa, pb, fl, it, s);
+        HIPCHECK(hipGetLastError());
+        iters = it + 1;
+      }
+      HIPCHECK(hipMemcpyAsync(x_out, dx, bytes, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      if (iters_out) *iters_out = iters;
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      for (void* p : bufs) (void)hipFree(p);
+      (void)hipStreamDestroy(s);
+      throw;
+    }
+    for (void* p : bufs) (void)hipFree(p);
+    HIPCHECK(hipStreamDestroy(s));
+  });
+}
+
+int trpo_linesearch(trpo_engine* e, const float* x, const float* fullstep, double rate,
+                    float* theta_out, int* k_out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && x && fullstep && theta_out, "NULL argument");
+    e->use();
+    const int64_t P = e->P;
+    e->copy_in(e->theta_prev, x, P * sizeof(float), mem);
+    e->copy_in(e->fullstep, fullstep, P * sizeof(float), mem);
+    // fval = f(x)  (utils.py:173)
+    e->eval_losses_dev(e->theta_prev);
+    e->fetch_scalars();
+    UpdScalars init = *e->hsc;
+    init.loss_before[0] = init.loss_trial[0];
+    init.loss_before[1] = init.loss_trial[1];
+    init.loss_before[2] = init.loss_trial[2];
+    init.rate = rate;
+    init.accepted = 0;
+    init.k = -1;
+    *e->hsc = init;
+    HIPCHECK(hipMemcpyAsync(e->sc, e->hsc, sizeof(UpdScalars), hipMemcpyHostToDevice, e->stream));
+    int k_acc = -1;
+    for (int k = 0; k < 10; ++k) {
+      launch_ls_trial(e->theta_prev, e->fullstep, e->theta_trial, P, k, e->sc, e->stream);
+      e->eval_losses_dev(e->theta_trial);
+      launch_ls_decide(e->sc, k, e->stream);
+      check_launch();
+      e->fetch_scalars();
+      HIPCHECK(hipMemcpyAsync(e->theta, e->theta_trial, P * sizeof(float), hipMemcpyDeviceToDevice,
+                              e->stream));   // loss() leaves sff(xnew) behind
+      if (e->hsc->accepted) {
+        k_acc = k;
+        break;
+      }
+    }
+    e->prepared = false;
+    e->copy_out(theta_out, k_acc >= 0 ? e->theta_trial : e->theta_prev, P * sizeof(float), mem);
+    if (k_out) *k_out = k_acc;
+  });
+}
+
+void trpo_default_params(trpo_update_params* p) {
+  if (!p) return;
+  p->cg_iters = 10;
+  p->residual_tol = 1e-10f;
+  p->cg_damping = 0.1f;
+  p->max_kl = 0.01;
+  p->compute_advantages = 0;
+  p->gamma = 0.95;
+}
+
+int trpo_update(trpo_engine* e, const trpo_update_params* p, trpo_update_stats* stats) {
+  return guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    trpo_update_params prm;
+    trpo_default_params(&prm);
+    if (p) prm = *p;
+    e->update(prm, stats);
+  });
+}
+
+int trpo_device_count(int* out) {
+  return guarded([&] {
+    REQUIRE(out, "NULL argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    (void)hipGetLastError();
+    *out = n;
+  });
+}
+
+int trpo_discount(const double* x, const uint8_t* starts, int64_t n, double gamma, double* out, int mem) {
+  return guarded([&] {
+    REQUIRE(x && out, "NULL argument");
+    REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return;
+    hipStream_t s = nullptr;
+    double *dx = nullptr, *dy = nullptr;
+    uint8_t* ds = nullptr;
+    void* ws = nullptr;
+    const bool dev = mem == TRPO_MEM_DEVICE;
+    HIPCHECK(hipMalloc(&ws, discount_workspace_bytes(n)));
+    if (!dev) {
+      HIPCHECK(hipMalloc(&dx, n * sizeof(double)));
+      HIPCHECK(hipMalloc(&dy, n * sizeof(double)));
+      HIPCHECK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipMalloc(&ds, n));
+    if (starts)
+      HIPCHECK(hipMemcpy(ds, starts, n, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    else
+      HIPCHECK(hipMemset(ds, 0, n));
+    launch_discount(dev ? x : dx, ds, n, gamma, dev ? out : dy, ws, s);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipDeviceSynchronize());
+    if (!dev) HIPCHECK(hipMemcpy(out, dy, n * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(ws);
+    (void)hipFree(ds);
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+  });
+}
+
+int trpo_profile_enable(trpo_engine* e, int enable) {
+  return guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    e->prof_collect();
+    e->prof = enable != 0;
+  });
+}
+
+int trpo_profile_reset(trpo_engine* e) {
+  return guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    e->prof_collect();
+    e->prof_acc.clear();
+  });
+}
+
+int trpo_profile_query(trpo_engine* e, char* buf, int cap) {
+  std::string js;
+  int rc = guarded([&] {
+    REQUIRE(e, "engine is NULL");
+    e->use();
+    e->prof_collect();
+    js = "{";
+    bool first = true;
+    for (auto& kv : e->prof_acc) {
+      char item[256];
+      std::snprintf(item, sizeof item, "%s\"%s\": [%ld, %.6f]", first ? "" : ", ", kv.first.c_str(),
+                    kv.second.first, kv.second.second);
+      js += item;
+      first = false;
+    }
+    js += "}";
+  });
+  if (rc != TRPO_OK) return rc;
+  if (buf && cap > 0) {
+    std::strncpy(buf, js.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = '\0';
+  }
+  return (int)js.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+// Host-side launch interface of the HIP kernels (gemm.hip, vec.hip, scan.hip).
+//
+// Everything here is stream-ordered and allocation-free, so a caller may capture
+// it into a hipGraph.  Pointers are device pointers.  Row-major activation
+// arrays have a leading dimension that is a multiple of 4 floats (16-B rows)
+// and zero-filled padding columns.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace trpo {
+
+// ---------------------------------------------------------------------------
+// Row GEMM:  C[M x N] = sum_seg A_seg[M x K_seg] * B_seg[K_seg x Npad]  -> epilogue
+// ---------------------------------------------------------------------------
+struct GemmSeg {
+  const float* A;  // [M][lda]
+  const float* B;  // [K][ldb]
+  int lda, ldb, K; // K multiple of 4
+};
+
+enum class RowEpi : int {
+  kTanh = 0,      // out = tanh(acc + bias)                      (policy forward, hidden)
+  kRHidden = 1,   // RH = (1-H^2)(acc + bias)                    (R-forward, hidden)
+  kPrepBwd = 2,   // D = acc(1-H^2); E = -2 acc H                (KL_ff plain backward)
+  kPgBwd = 3,     // DS = acc(1-H^2)                             (surr backward)
+  kRBwd = 4,      // RD = acc(1-H^2) + E RH                      (R-backward)
+  kPrepHead = 5,  // softmax head: P, D_L, DS_L, row loss terms  (prepare)
+  kLossHead = 6,  // softmax head: row loss terms only           (line search)
+  kRHead = 7,     // R-softmax head: RD_L                        (FVP)
+};
+
+struct RowEpiArgs {
+  const float* bias;   // [N] (kTanh, kRHidden, heads)
+  const float* H;      // [M][ldo] tanh activation at the output position
+  const float* E;      // [M][ldo]
+  const float* RH;     // [M][ldo]
+  float* out0;         // tanh: H ; RHidden: RH ; PrepBwd: D ; PgBwd: DS ; RBwd: RD ; heads: P/RD_L
+  float* out1;         // PrepBwd: E ; PrepHead: D_L
+  float* out2;         // PrepHead: DS_L
+  int ldo;             // leading dim of outputs/aux (multiple of 4)
+  // heads
+  const float* P;      // kRHead: cached softmax [M][ldo]
+  const float* old;    // [M][ldo]
+  const int* act;      // [M]
+  const float* adv;    // [M]
+  double* rowterms;    // [M][4] (surr*N, kl*N, ent*N, -)
+  double invN;         // 1 / N_global
+};
+
+struct RowGemmArgs {
+  int M, N, Npad;      // rows; real output columns; padded output columns (<= ldb)
+  int nseg;
+  GemmSeg seg[2];
+  const int* skip;     // optional device flag: launch is a no-op when *skip != 0
+  RowEpi epi;
+  RowEpiArgs ea;
+};
+
+void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Weight-gradient GEMM (split-K over rows):
+//   slab[split][off_w + i*Nb + j] = sum_seg sum_rows A_seg[r][i] B_seg[r][j]
+//   slab[split][off_b + j]        = sum_rows B_{colsum_seg}[r][j]
+// ---------------------------------------------------------------------------
+struct WSeg {
+  const float* A;  // [rows][lda]
+  const float* B;  // [rows][ldb]
+  int lda, ldb;
+};
+
+struct WGradArgs {
+  int rows;
+  int Ma, Nb;          // real output dims (fan_in, fan_out)
+  int Mpad, Npad;      // padded widths of A / B rows
+  int nseg;
+  WSeg seg[2];
+  int colsum_seg;      // B of this segment is column-summed into the bias slot
+  int splits, rows_per_split;  // rows_per_split multiple of 16
+  float* slab;
+  int64_t slab_stride; // floats between consecutive splits
+  int64_t off_w, off_b;
+  const int* skip;
+};
+
+void launch_wgrad(const WGradArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// vector / scalar kernels (vec.hip)
+// ---------------------------------------------------------------------------
+struct LayerPack {
+  int64_t off_w;   // offset of W_l [a x b] in the flat vector
+  int a, b, apad, bpad;
+  float* WF;       // [2*apad][bpad]: rows [0,a) = W ; rows [apad, apad+a) = V
+  float* WB;       // [2*bpad][apad]: rows [0,b) = W^T ; rows [bpad, bpad+b) = V^T
+};
+constexpr int kMaxLayers = 8;
+struct PackArgs {
+  int nl;
+  LayerPack L[kMaxLayers];
+};
+// which = 0: source is theta -> W halves ; which = 1: source is a tangent -> V halves
+void launch_pack(const PackArgs& pa, const float* src, int which, const int* skip, hipStream_t s);
+
+// out[p] = sum_{s<S} slab[s*stride + p]
+void launch_reduce_slab(const float* slab, int S, int64_t stride, int64_t P, float* out,
+                        const int* skip, hipStream_t s);
+
+// Device scalar state of one update (CG, step scaling, line search).
+struct UpdScalars {
+  float rdotr[2];     // CG ping-pong (utils.py:189,198)
+  float alpha, mu;
+  int iters;          // CG iterations run
+  int pad0;
+  float tol;
+  float damping;
+  // step scaling (trpo_inksci.py:148-151)
+  float sdotz;        // stepdir . fvp(stepdir)
+  float gdots;        // g . stepdir
+  double shs, lm, rate;
+  // losses (f32 like session.run)
+  float loss_before[3];
+  float loss_trial[3];
+  float loss_after[3];
+  int accepted, k, reverted, pad1;
+  double max_kl;
+};
+constexpr int kMaxCG = 64;
+struct CGFlags {
+  int done[kMaxCG + 2];  // done[i] is read by iteration i, written by iteration i-1
+};
+
+void launch_dot_partials(const float* a, const float* b, int64_t n, double* partials,
+                         const int* skip, hipStream_t s);
+// CG of utils.py:185-201.  init: x = 0, r = b, p = b, rdotr = f32(b.b), flags cleared.
+// iter `it` (no-op once done[it] is set): z = hv + damping p ; alpha = rdotr/(p.z) ;
+// x += alpha p ; r -= alpha z ; mu = (r.r)/rdotr ; p = r + mu p ; done[it+1] = r.r < tol.
+void launch_cg_init(const float* b, float* x, float* r, float* p, int64_t n, double* partials,
+                    UpdScalars* sc, CGFlags* fl, float tol, float damping, hipStream_t s);
+void launch_cg_iter(const float* hv, float* x, float* r, float* p, float* z, int64_t n, UpdScalars* sc,
+                    double* partials, double* partials2, CGFlags* fl, int it, hipStream_t s);
+struct CGScalarsD {
+  double rdotr[2];
+  double alpha, mu;
+  int iters, pad;
+  double tol, damping;
+};
+void launch_cg_init_d(const double* b, double* x, double* r, double* p, int64_t n, double* partials,
+                      CGScalarsD* sc, CGFlags* fl, double tol, hipStream_t s);
+void launch_cg_iter_d(const double* hv, double* x, double* r, double* p, double* z, int64_t n,
+                      CGScalarsD* sc, double* partials, double* partials2, CGFlags* fl, int it,
+                      hipStream_t s);
+
+// z = hv + damping*stepdir; partials = stepdir.z ; partials2 = g.stepdir
+void launch_shs_partials(const float* hv, const float* stepdir, const float* g, int64_t n,
+                         const UpdScalars* sc, double* partials, double* partials2, hipStream_t s);
+// shs, lm, rate (single block)
+void launch_shs_finish(const double* partials, const double* partials2, UpdScalars* sc, hipStream_t s);
+// fullstep = stepdir / f32(lm)
+void launch_fullstep(const float* stepdir, float* fullstep, int64_t n, const UpdScalars* sc, hipStream_t s);
+// trial = prev + f32(0.5^k) * fullstep (no-op when accepted)
+void launch_ls_trial(const float* prev, const float* fullstep, float* trial, int64_t n, int k,
+                     const UpdScalars* sc, hipStream_t s);
+
+// row loss terms -> kRedBlocks partial triples
+void launch_rowterms_partials(const double* rowterms, int64_t n, double* partials3,
+                              const int* skip, hipStream_t s);
+// local[0..2] = ordered sum of the partial triples
+void launch_rowterms_finish(const double* partials3, double* local3, const int* skip, hipStream_t s);
+// which: 0 -> loss_before, 1 -> loss_trial ; out3 = f32(-sum_surr/N, sum_kl/N, sum_ent/N)
+void launch_losses_store(const double* global3, double invN, UpdScalars* sc, int which,
+                         const int* skip, hipStream_t s);
+// line search decision for backtrack k (utils.py:176-181)
+void launch_ls_decide(UpdScalars* sc, int k, hipStream_t s);
+// theta = accepted ? prev + 0.5^k fullstep : prev ; revert if kl > 2 max_kl (trpo_inksci.py:153-158)
+void launch_ls_finalize(const float* prev, const float* fullstep, float* theta, float* theta_ls,
+                        int64_t n, UpdScalars* sc, hipStream_t s);
+
+void launch_axpby(float* y, const float* x, float alpha, float beta, int64_t n, hipStream_t s);  // y = alpha*x + beta*y
+void launch_scale_copy(const float* x, float* y, float alpha, int64_t n, hipStream_t s);          // y = alpha*x
+void launch_i64_to_i32(const int64_t* src, int* dst, int64_t n, int* bad, int hi, hipStream_t s);
+void launch_copy_rows(const float* src, int64_t n, int w, int ld_src, float* dst, int ld_dst, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// discount scan + standardisation (scan.hip)
+// ---------------------------------------------------------------------------
+// out[t] = x[t] + gamma*out[t+1] within episodes (starts[t] = 1 begins an episode)
+size_t discount_workspace_bytes(int64_t n);
+void launch_discount(const double* x, const uint8_t* starts, int64_t n, double gamma, double* out,
+                     void* workspace, hipStream_t s);
+// adv = returns - baseline ; partials = sum adv
+void launch_adv_center_partials(const double* returns, const double* baseline, double* adv,
+                                int64_t n, double* partials, hipStream_t s);
+void launch_sum_finish(const double* partials, double* out, hipStream_t s);  // out[0] = ordered sum
+// partials = sum (adv - mean)^2 with mean = global_sum[0] * inv_n
+void launch_adv_sq_partials(const double* adv, int64_t n, const double* global_sum, double inv_n,
+                            double* partials, hipStream_t s);
+// adv = (adv - mean)/(sqrt(sq*inv_n) + 1e-8) ; adv32 = f32(adv)
+void launch_adv_normalize(double* adv, float* adv32, int64_t n, const double* global_sum,
+                          const double* global_sq, double inv_n, hipStream_t s);
+
+}  // namespace trpo
