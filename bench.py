@@ -1,0 +1,275 @@
+#!/usr/bin/env python
+"""bench.py — TRPO policy-update throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One *step* = one full TRPO update of BASELINE.json's metric ("10-iter CG +
+linesearch") over the synthetic batch, exactly the unit of SURVEY.md §8(d):
+discount + standardise + policy gradient + 10 CG iterations (residual_tol = 0,
+so all 10 run) + the shs FVP + line search + final losses / revert check.
+Inputs are resident in HBM before the timed region.  Each step restarts from
+the same theta_0 (a device-to-device copy of P floats) so every step does the
+same work (steady state: pi_old = p(theta_0)).
+
+Default workload (N=1 and the scaling runs): C4 = 8,000,000 states, obs 128,
+256x256 tanh MLP, 18 actions (BASELINE.json configs[3]); with N ranks the 8M
+states are split row-wise (path-aligned), so ``scaling`` is "strong".
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel (largest
+share of HIP-event time over the timed region, on the engine's stream):
+algorithmic FLOPs per launch / average launch time vs the f32 MFMA peak.
+``cpu_baseline`` (N=1, rank 0 only) times the TF-faithful float32 CPU mirror of
+the reference (oracle/tf_graph_torch.py: every FVP recomputes forward + both
+backward passes, as each session.run does) on a bounded row sample and
+extrapolates linearly in N (every op of the update is O(N)).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "TRPO updates/sec (10-iter CG + linesearch) at N states; FVP GB/s vs HBM peak"
+PEAK_F32_TFLOPS = 157.3        # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+EPISODE_LEN = 200              # CartPole-v0 cap
+
+CONFIGS = {
+    "c2": dict(n=50_000, obs=11, hidden=[64, 64], A=3, cpu_rows=50_000,
+               name="C2: 50k states, obs 11, 64x64 tanh MLP, 3 actions"),
+    "c3": dict(n=1_000_000, obs=128, hidden=[64, 64], A=18, cpu_rows=100_000,
+               name="C3: 1M states, obs 128, 64x64 tanh MLP, 18 actions"),
+    "c4": dict(n=8_000_000, obs=128, hidden=[256, 256], A=18, cpu_rows=60_000,
+               name="C4: 8M states, obs 128, 256x256 tanh MLP, 18 actions"),
+    "c5": dict(n=4_000_000, obs=376, hidden=[1024, 1024], A=17, cpu_rows=4_000,
+               name="C5: 4M states, obs 376, 1024x1024 tanh MLP, 17 actions"),
+}
+
+
+def tag_flops(tag: str, widths, n: int) -> float:
+    """Algorithmic FLOPs of one launch of the kernel behind a profile tag."""
+    role, _, l = tag.rpartition("_l")
+    if not l.isdigit():
+        return 0.0
+    l = int(l)
+    a, b = widths[l], widths[l + 1]
+    ab = 2.0 * n * a * b
+    if role in ("fwd", "ls_fwd", "bwd", "pg_bwd", "pg_wgrad"):
+        return ab
+    if role in ("fvp_rfwd", "fvp_wgrad"):
+        return ab if l == 0 else 2 * ab
+    if role == "fvp_rbwd":
+        return 2 * ab
+    return 0.0
+
+
+def fvp_flops_per_row(widths) -> float:
+    """4 a1 b1 + 12 sum_{l>=2} a_l b_l."""
+    f = 0.0
+    for l in range(len(widths) - 1):
+        ab = widths[l] * widths[l + 1]
+        f += 4 * ab if l == 0 else 12 * ab
+    return f
+
+
+def synthetic_theta(widths, rng) -> np.ndarray:
+    """W ~ U(+-sqrt(6/(fan_in+fan_out))), b ~ N(0, 0.1^2), flat [W1,b1,...]."""
+    parts = []
+    for a, b in zip(widths[:-1], widths[1:]):
+        lim = (6.0 / (a + b)) ** 0.5
+        parts.append(rng.uniform(-lim, lim, size=a * b))
+        parts.append(rng.normal(0.0, 0.1, size=b))
+    return np.concatenate(parts).astype(np.float32)
+
+
+def cpu_baseline(cfg, rows: int, threads: int):
+    """TF-faithful float32 CPU update on `rows` states; returns a cpu_baseline dict."""
+    import torch
+    from oracle import trpo_oracle as O
+    from oracle.tf_graph_torch import TFFaithfulCPU
+    torch.set_num_threads(threads)
+    spec = O.PolicySpec(cfg["obs"], cfg["hidden"], cfg["A"])
+    # warm the torch CPU kernels on a small batch (allocator / thread pool start-up)
+    small = O.synthetic_batch(spec, 512, seed=11)
+    TFFaithfulCPU(spec, small["X"], small["actions"], small["advant"], small["old_dist"],
+                  small["theta"]).update(cg_iters=2, residual_tol=0.0)
+    d = O.synthetic_batch(spec, rows, seed=12, episode_len=EPISODE_LEN)
+    mirror = TFFaithfulCPU(spec, d["X"], d["actions"], d["advant"], d["old_dist"], d["theta"])
+    t0 = time.perf_counter()
+    ret = O.discount_segmented(d["rewards"], d["starts"], 0.95)       # discount + standardise too
+    O.standardize(ret)
+    mirror.update(cg_iters=10, residual_tol=0.0)
+    dt = time.perf_counter() - t0
+    per_update_full = dt * cfg["n"] / rows
+    return {"value": 1.0 / per_update_full, "unit": "updates/s", "cores": threads, "kind": "port",
+            "sample": f"one full update (10 CG iters, residual_tol=0) on {rows:,} of the {cfg['n']:,} states "
+                      f"({dt:.2f} s), TF-faithful torch-CPU fp32 mirror, extrapolated linearly in N"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=0, help="override total states (testing only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=0)
+    ap.add_argument("--profile-out", default="", help="write the per-tag HIP-event profile here (JSON)")
+    args = ap.parse_args()
+
+    cfg = dict(CONFIGS[args.config])
+    if args.rows:
+        cfg["n"] = args.rows
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd.dist import init_engine_comm, shard_bounds
+
+    N = cfg["n"]
+    widths = [cfg["obs"], *cfg["hidden"], cfg["A"]]
+    starts_all = None   # episodes every EPISODE_LEN rows -> shard cuts on path starts
+    bounds = shard_bounds(N, world, (np.arange(N) % EPISODE_LEN == 0) if N <= 50_000_000 else starts_all)
+    lo, hi = bounds[rank]
+    n = hi - lo
+
+    eng = Engine(cfg["obs"], cfg["hidden"], cfg["A"], max_rows=max(n, 16), device=local_rank)
+    init_engine_comm(eng, rank, world)
+
+    # ---- synthetic inputs, generated on the device ----
+    theta0 = synthetic_theta(widths, np.random.RandomState(0))
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    X = torch.randn((n, cfg["obs"]), generator=g, device=dev, dtype=torch.float32)
+    actions = torch.randint(0, cfg["A"], (n,), generator=g, device=dev, dtype=torch.int64)
+    rewards = torch.rand((n,), generator=g, device=dev, dtype=torch.float64)
+    starts = ((torch.arange(lo, hi, device=dev) % EPISODE_LEN) == 0).to(torch.uint8)
+    uniform = torch.full((n, cfg["A"]), 1.0 / cfg["A"], device=dev, dtype=torch.float32)
+    zeros = torch.zeros((n,), device=dev, dtype=torch.float32)
+    eng.set_flat(theta0)
+    eng.set_batch(X, actions, zeros, uniform, n_global=N)
+    old = torch.empty((n, cfg["A"]), device=dev, dtype=torch.float32)
+    eng.action_dist(out=old)                       # steady state: pi_old = p(theta_0)
+    eng.set_batch(X, actions, zeros, old, n_global=N)
+    eng.set_rewards(rewards, starts)
+    del uniform, X
+    theta0_dev = torch.from_numpy(theta0).to(dev)
+    params = UpdateParams(cg_iters=10, residual_tol=0.0, cg_damping=0.1, max_kl=0.01,
+                          compute_advantages=True, gamma=0.95)
+
+    last = {}
+
+    def step():
+        eng.set_flat(theta0_dev)
+        last.update(eng.update(params))
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    eng.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    eng.profile_reset()
+    eng.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = eng.profile_query()
+    eng.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if args.profile_out and rank == 0:
+        with open(args.profile_out, "w") as f:
+            json.dump({"profile": prof, "steps": args.steps, "n_local": n, "widths": widths}, f, indent=1)
+
+    if rank == 0:
+        # ---- roofline of the dominant kernel (HIP events on the engine stream) ----
+        kernel_tags = {t: v for t, v in prof.items() if tag_flops(t, widths, n) > 0}
+        dom = max(kernel_tags, key=lambda t: kernel_tags[t][1])
+        cnt, tot_ms = kernel_tags[dom]
+        avg_s = tot_ms / cnt / 1e3
+        fl = tag_flops(dom, widths, n)
+        achieved = fl / avg_s / 1e12
+        upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / args.steps
+        upd_s = elapsed / args.steps
+        fvp_ms = sum(ms for t, (c, ms) in prof.items() if t.startswith("fvp_") or t == "reduce")
+        fvp_calls = prof.get("fvp_wgrad_l0", [0, 0])[0]
+        fvp_s = fvp_ms / max(1, fvp_calls) / 1e3 if fvp_calls else float("nan")
+        fvp_bytes = n * cfg["obs"] * 4 + 3 * eng.num_params * 4
+        out = {
+            "metric": METRIC,
+            "value": args.steps / elapsed,
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (X~N(0,1), a~U{0..A-1}, rewards~U(0,1), paths of 200 steps, "
+                    "random-init policy, pi_old = p(theta_0))",
+            "config": {"workload": cfg["name"] + "; full update = discount+standardise+pg+10 CG+shs FVP+"
+                                                 "line search+final losses",
+                       "n_states": N, "obs_dim": cfg["obs"], "hidden": cfg["hidden"], "n_actions": cfg["A"],
+                       "num_params": eng.num_params, "cg_iters": 10, "residual_tol": 0.0,
+                       "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_F32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                         "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt},
+            "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
+                                "achieved_tflops": upd_flops * world / upd_s / 1e12,
+                                "frac_of_peak": upd_flops / upd_s / 1e12 / PEAK_F32_TFLOPS},
+            "fvp": {"ms_per_fvp": fvp_s * 1e3, "gbps_algorithmic": fvp_bytes / fvp_s / 1e9,
+                    "hbm_frac": fvp_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
+                    "tflops": fvp_flops_per_row(widths) * n / fvp_s / 1e12},
+            "last_update": {k: last[k] for k in ("cg_iters", "k", "reverted", "kl_after", "surr_after")},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+                threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+            rows = args.cpu_rows or min(cfg["cpu_rows"], N)
+            out["cpu_baseline"] = cpu_baseline(cfg, rows, threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

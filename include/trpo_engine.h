@@ -120,6 +120,9 @@ int trpo_compute_advantages(trpo_engine* e, double gamma, double* returns_out, d
 int trpo_losses(trpo_engine* e, float out3[3]);
 /* loss(th): SetFromFlat(th) then session.run(surr) (trpo_inksci.py:127-129); out3 = [surr, kl, ent] */
 int trpo_eval_losses(trpo_engine* e, const float* theta, float out3[3], int mem);
+/* session.run(self.action_dist) -> [n][n_actions] f32 at the current parameters
+ * (trpo_inksci.py:38-40,78; the policy forward) */
+int trpo_action_dist(trpo_engine* e, float* out, int mem);
 /* session.run(self.pg) = flatgrad(surr, var_list) (trpo_inksci.py:54,146) */
 int trpo_policy_grad(trpo_engine* e, float* g_out, int mem);
 /* fisher_vector_product(p) = session.run(self.fvp) + cg_damping * p (trpo_inksci.py:56-70,124-126) */

@@ -57,6 +57,7 @@ SIGNATURES = {
     "trpo_compute_advantages": (c_int, [c_void_p, c_double, c_void_p, c_void_p, c_int]),
     "trpo_losses": (c_int, [c_void_p, POINTER(c_float)]),
     "trpo_eval_losses": (c_int, [c_void_p, c_void_p, POINTER(c_float), c_int]),
+    "trpo_action_dist": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_policy_grad": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_fvp": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_int]),
     "trpo_cg": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, POINTER(c_int), c_int]),

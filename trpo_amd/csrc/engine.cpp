@@ -375,7 +375,9 @@ struct trpo_engine {
         a.ea.rowterms = rowterms;
         a.ea.invN = 1.0 / (double)n_global;
       }
-      Scope sp(this, tag);
+      char t[32];
+      std::snprintf(t, sizeof t, "%s_l%d", tag, l);
+      Scope sp(this, t);
       launch_rowgemm(a, stream);
       check_launch();
     }
@@ -409,7 +411,9 @@ struct trpo_engine {
       a.ea.out0 = D[l - 1];
       a.ea.out1 = E[l - 1];
       a.ea.ldo = wp[l];
-      Scope sp(this, "bwd");
+      char t[32];
+      std::snprintf(t, sizeof t, "bwd_l%d", l);
+      Scope sp(this, t);
       launch_rowgemm(a, stream);
       check_launch();
     }
@@ -465,12 +469,17 @@ struct trpo_engine {
       a.ea.H = H[l];
       a.ea.out0 = DS[l - 1];
       a.ea.ldo = wp[l];
-      Scope sp(this, "pg_bwd");
+      char t[32];
+      std::snprintf(t, sizeof t, "pg_bwd_l%d", l);
+      Scope sp(this, t);
       launch_rowgemm(a, stream);
       check_launch();
     }
-    for (int l = 0; l < L; ++l)
-      wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1]}, WSeg{}, 0, nullptr, "pg_wgrad");
+    for (int l = 0; l < L; ++l) {
+      char t[32];
+      std::snprintf(t, sizeof t, "pg_wgrad_l%d", l);
+      wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1]}, WSeg{}, 0, nullptr, t);
+    }
     reduce_grad(g, nullptr);
   }
 
@@ -838,6 +847,22 @@ int trpo_eval_losses(trpo_engine* e, const float* theta, float out3[3], int mem)
     e->eval_losses_dev(e->theta);
     e->fetch_scalars();
     std::memcpy(out3, e->hsc->loss_trial, 3 * sizeof(float));
+  });
+}
+
+int trpo_action_dist(trpo_engine* e, float* out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && out, "NULL argument");
+    e->use();
+    e->prepare();
+    const int A = e->w[e->L];
+    float* tmp = nullptr;
+    HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)e->n * A * sizeof(float), e->stream));
+    launch_copy_rows(e->Pm, e->n, A, e->wp[e->L], tmp, A, e->stream);
+    check_launch();
+    e->copy_out(out, tmp, (size_t)e->n * A * sizeof(float), mem);
+    HIPCHECK(hipFreeAsync(tmp, e->stream));
+    HIPCHECK(hipStreamSynchronize(e->stream));
   });
 }
 

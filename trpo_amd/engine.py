@@ -193,6 +193,16 @@ class Engine:
         check(lib.trpo_eval_losses(self._h, t.ptr, out, t.mem), "trpo_eval_losses")
         return np.array(out[:], np.float32)
 
+    def action_dist(self, out=None):
+        """session.run(action_dist): the policy's softmax at the current parameters, [n, A]."""
+        if out is None:
+            res = np.empty((self.n, self.n_actions), np.float32)
+            a = _Arg(res, np.float32, writable=True)
+        else:
+            res, a = out, _Arg(out, np.float32, shape=(self.n, self.n_actions), writable=True)
+        check(lib.trpo_action_dist(self._h, a.ptr, a.mem), "trpo_action_dist")
+        return res
+
     def policy_grad(self, out=None):
         res, a = self._out(out, np.float32, self.num_params)
         check(lib.trpo_policy_grad(self._h, a.ptr, a.mem), "trpo_policy_grad")
