@@ -69,6 +69,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return ab if l == 0 else 2 * ab
     if role == "fvp_rbwd":
         return 2 * ab
+    if role == "fvp_head":          # R-forward (2ab) + R-backward (2ab) + wgrad (2ab) of the last layer
+        return 3 * ab
     return 0.0
 
 

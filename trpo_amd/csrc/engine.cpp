@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -127,6 +128,7 @@ struct trpo_engine {
   UpdScalars* hsc = nullptr;   // pinned host mirror
 
   bool prepared = false;
+  bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel
 
   // profiling
   bool prof = false;
@@ -272,6 +274,8 @@ struct trpo_engine {
     sc = dalloc<UpdScalars>(1);
     fl = dalloc<CGFlags>(1);
     dbad = dalloc<int>(1);
+    fused_head = L >= 2 && wp[L - 1] <= 256 && wp[L - 1] % 16 == 0 && wp[L] <= 32 &&
+                 std::getenv("TRPO_FUSED_HEAD") != nullptr;   // opt-in: slower than 3 kernels at C4 (1 block/CU)
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
     HIPCHECK(hipStreamSynchronize(stream));
@@ -492,7 +496,8 @@ struct trpo_engine {
       check_launch();
     }
     // R-forward
-    for (int l = 0; l < L; ++l) {
+    const int Lf = fused_head ? L - 1 : L;
+    for (int l = 0; l < Lf; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       float* Vpart = WF[l] + (size_t)wp[l] * wp[l + 1];
       if (l == 0) {
@@ -522,8 +527,39 @@ struct trpo_engine {
       launch_rowgemm(a, stream);
       check_launch();
     }
+    if (fused_head) {
+      HeadArgs h{};
+      const int l = L - 1;
+      h.rows = (int)n;
+      h.a = w[l];
+      h.b = w[l + 1];
+      h.apad = wp[l];
+      h.bpad = wp[l + 1];
+      h.RH = RH[l];
+      h.H = H[l];
+      h.WF = WF[l];
+      h.WB = WB[l];
+      h.c = v + offb[l];
+      h.P = Pm;
+      h.DL = D[l];
+      h.E = E[l - 1];
+      h.RDout = RD[l - 1];
+      h.invN = 1.0 / (double)n_global;
+      h.splits = active_splits;
+      h.rows_per_split = rows_per_split;
+      h.slab = slab;
+      h.slab_stride = slab_stride;
+      h.off_w = offW[l];
+      h.off_b = offb[l];
+      h.skip = skip;
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_head_l%d", l);
+      Scope sp(this, tag);
+      launch_fvp_head(h, stream);
+      check_launch();
+    }
     // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
-    for (int l = L - 1; l >= 1; --l) {
+    for (int l = fused_head ? L - 2 : L - 1; l >= 1; --l) {
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 2;
       a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
@@ -542,7 +578,7 @@ struct trpo_engine {
       check_launch();
     }
     // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < Lf; ++l) {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
       if (l == 0)

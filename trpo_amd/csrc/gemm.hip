@@ -21,6 +21,7 @@
 // to 4h + s for k-step s, so A fragments come from one ds_read_b128.
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -74,6 +75,34 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
   }
 }
 
+// value part (loads + math) and store part of the element-wise epilogues.
+// No column predicate: padding columns (col >= N) have zero accumulators (zero
+// weight padding), zero bias and zero H/E/RH padding, so every formula below
+// already yields exactly 0 there.  Loads are therefore unconditional and hipcc
+// keeps them all in flight (a `cond ? load : 0` becomes a branch per load).
+template <int EPI>
+__device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool /*real*/, float v, float bv,
+                                           float& o0, float& o1) {
+  if constexpr (EPI == (int)RowEpi::kTanh) {
+    o0 = tanhf(v + bv);
+  } else if constexpr (EPI == (int)RowEpi::kRHidden) {
+    o0 = one_minus_sq(e.H[idx]) * (v + bv);
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
+    const float h = e.H[idx];
+    o0 = v * one_minus_sq(h);
+    o1 = -2.0f * v * h;
+  } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
+    o0 = v * one_minus_sq(e.H[idx]);
+  } else if constexpr (EPI == (int)RowEpi::kRBwd) {
+    o0 = fmaf(e.E[idx], e.RH[idx], v * one_minus_sq(e.H[idx]));
+  }
+}
+template <int EPI>
+__device__ __forceinline__ void epi_store(const RowEpiArgs& e, size_t idx, float o0, float o1) {
+  e.out0[idx] = o0;
+  if constexpr (EPI == (int)RowEpi::kPrepBwd) e.out1[idx] = o1;
+}
+
 // ---------------------------------------------------------------------------
 // row-wise softmax-head epilogues.  The 32 columns of one row live on the 32
 // lanes of one wave half (col = lane & 31); reductions are xor-shuffles of
@@ -82,21 +111,28 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
 template <int EPI>
 __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowvalid, int col, int A,
                                         float v) {
+  // `row` is already clamped into [0, M); loads go to clamped (valid) addresses
+  // unconditionally and are masked by selects, so hipcc keeps them in flight.
   const bool real = col < A;
-  const size_t idx = (size_t)row * e.ldo + col;
+  const int colc = col < e.ldo ? col : e.ldo - 1;
+  const size_t idx = (size_t)row * e.ldo + colc;
   const bool st = rowvalid && col < e.ldo;
   if constexpr (EPI == (int)RowEpi::kPrepHead || EPI == (int)RowEpi::kLossHead) {
+    const float bias = e.bias[real ? col : 0];
+    const float oldv = e.old[idx];
+    const int av = e.act[row];
+    const float advv = e.adv[row];
     // p = softmax(z)   (trpo_inksci.py:40)
-    const float z = real ? v + e.bias[col] : -INFINITY;
+    const float z = real ? v + bias : -INFINITY;
     const float m = hmax32(z);
     const float ex = real ? expf(z - m) : 0.0f;
     const float ssum = hsum32(ex);
     const float p = ex / ssum;
-    const int a = rowvalid ? e.act[row] : 0;
-    const float old = (rowvalid && real) ? e.old[idx] : 0.0f;
+    const int a = rowvalid ? av : 0;
+    const float old = (rowvalid && real) ? oldv : 0.0f;
     const float pa = __shfl(p, a, 32);
     const float olda = __shfl(old, a, 32);
-    const float adv = rowvalid ? e.adv[row] : 0.0f;
+    const float adv = rowvalid ? advv : 0.0f;
     const double pd = p, od = old;
     // row loss terms (:46-51), accumulated in f64
     const double klt = hsum32d(real ? od * log((od + (double)kEps) / (pd + (double)kEps)) : 0.0);
@@ -109,7 +145,8 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
       e.rowterms[4 * (size_t)row + 3] = 0.0;
     }
     if constexpr (EPI == (int)RowEpi::kPrepHead) {
-      if (st) e.out0[idx] = real ? p : 0.0f;
+      const size_t sidx = (size_t)row * e.ldo + col;
+      if (st) e.out0[sidx] = real ? p : 0.0f;
       // KL_ff plain logit delta (:56-57), cancellation-free:
       //   d_j = (p_j/N) (B_j - sum_k p_k B_k),  B = eps/(p+eps)
       const double B = real ? (double)kEps / (pd + (double)kEps) : 0.0;
@@ -120,8 +157,8 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
       const double coef = -(double)adv * e.invN / (double)olda * (double)pa;
       const double ds = real ? coef * (col == a ? rest : -pd) : 0.0;
       if (st) {
-        e.out1[idx] = (float)dl;
-        e.out2[idx] = (float)ds;
+        e.out1[sidx] = (float)dl;
+        e.out2[sidx] = (float)ds;
       }
     }
   } else if constexpr (EPI == (int)RowEpi::kRHead) {
@@ -129,8 +166,10 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     //   Rp   = p (Rz - <p,Rz>)
     //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k]
     //   A = p/(p+eps), B = eps/(p+eps)
-    const double rz = real ? (double)(v + e.bias[col]) : 0.0;
-    const double pd = (rowvalid && real) ? (double)e.P[idx] : 0.0;
+    const float bias = e.bias[real ? col : 0];
+    const float pv = e.P[idx];
+    const double rz = real ? (double)(v + bias) : 0.0;
+    const double pd = (rowvalid && real) ? (double)pv : 0.0;
     const double prz = hsum32d(pd * rz);
     const double Rp = pd * (rz - prz);
     const double den = pd + (double)kEps;
@@ -139,12 +178,24 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     const double spB = hsum32d(pd * B);
     const double sRAB = hsum32d(Rp * Aa * B);
     const double rd = e.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
-    if (st) e.out0[idx] = real ? (float)rd : 0.0f;
+    if (st) e.out0[(size_t)row * e.ldo + col] = real ? (float)rd : 0.0f;
   }
 }
 
-template <int WM, int WN, int TM, int TN, int EPI>
-__global__ void __launch_bounds__(WM* WN * 64)
+// Linear block id -> (m-tile, n-tile).  The n-tiles of one row tile are adjacent in
+// the swizzled order and land on one XCD (blocks b and b+8 share an XCD under the
+// observed round-robin dispatch: speed only, never correctness), so the second
+// n-tile re-reads the A rows from that XCD's L2.
+__device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
+  const int id = blockIdx.x, nwg = gridDim.x;
+  int swz = id;
+  if ((nwg & 7) == 0) swz = (id & 7) * (nwg >> 3) + (id >> 3);
+  mt = swz / ntn;
+  nt = swz - mt * ntn;
+}
+
+template <int WM, int WN, int TM, int TN, int BK, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64, EPI == 2 ? 2 : 4)   // 4 waves / SIMD: <= 128 VGPRs
 rowgemm_kernel(const RowGemmArgs args) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int LDA = BK + 4;   // A tile [BM][BK+4]: conflict-free ds_read_b128 column groups
@@ -156,7 +207,9 @@ rowgemm_kernel(const RowGemmArgs args) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mt, ntile;
+  tile_of((args.Npad + BN - 1) / BN, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
   const int M = args.M;
 
   const int nt0 = (args.seg[0].K + BK - 1) / BK;
@@ -186,20 +239,19 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       const int r = f / (BK / 4), kq = f % (BK / 4);
       const int row = m0 + r, k = k0 + 4 * kq;
-      f32x4 v = f32x4{};
-      if ((AF4 % NT == 0 || f < AF4) && row < M && k < K)
-        v = *reinterpret_cast<const f32x4*>(Ap + (size_t)row * lda + k);
-      ra[i] = v;
+      // branch-free guard: always load from a clamped (valid) address, select zero
+      const bool ok = (AF4 % NT == 0 || f < AF4) && row < M && k < K;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
+      ra[i] = ok ? v : f32x4{};
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
       const int f = tid + i * NT;
       const int kr = f / (BN / 4), cq = f % (BN / 4);
       const int k = k0 + kr, col = n0 + 4 * cq;
-      f32x4 v = f32x4{};
-      if ((BF4 % NT == 0 || f < BF4) && k < K && col < args.Npad)
-        v = *reinterpret_cast<const f32x4*>(Bp + (size_t)k * ldb + col);
-      rb[i] = v;
+      const bool ok = (BF4 % NT == 0 || f < BF4) && k < K && col < args.Npad;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? k : 0) * ldb + (ok ? col : 0));
+      rb[i] = ok ? v : f32x4{};
     }
   };
   auto sstore = [&](int buf) {
@@ -272,18 +324,96 @@ rowgemm_kernel(const RowGemmArgs args) {
         epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r]);
       }
   } else {
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+    const bool fulln = (n0 + BN <= args.Npad);
+    if (fulln) {
+      // Full-width tile: every epilogue operand goes through a per-block buffer
+      // descriptor (base = row m0, num_records = the rows this tile owns), so a
+      // load/store is one buffer op with a lane-constant voffset and a per-row SGPR
+      // soffset; rows past M fall outside the descriptor (loads read 0, stores are
+      // dropped) -- no per-element predicate, no 64-bit address math, and all 16
+      // loads of a chunk stay in flight.
+      const int ldo = e.ldo;
+      const int Mt = M - m0 < BM ? M - m0 : BM;
+      const int tile_bytes = Mt * ldo * 4;
+      auto mk = [&](const float* ptr) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
+      };
+      constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
+                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd;
+      constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
+      constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd;
+      // descriptors of operands an epilogue does not use alias out0 and are never touched
+      const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
+      const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
+      const __amdgpu_buffer_rsrc_t rE = mk(kRB ? e.E : e.out0);
+      const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
+      const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
+      const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
+      auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+      };
+      auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+      };
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int col = n0 + wn * TN * 32 + tn * 32 + lr;
-        if (col >= args.Npad) continue;
+        float bv = 0.0f;
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden)
+          bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
+        const int vo = vbase + tn * 128;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < M) epi_elem<EPI>(e, row, col, col < args.N, acc[tm][tn][r]);
+        for (int tm = 0; tm < TM; ++tm) {
+          float o0[16], o1[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+            const float v = acc[tm][tn][r];
+            if constexpr (EPI == (int)RowEpi::kTanh) {
+              o0[r] = tanhf(v + bv);
+            } else if constexpr (EPI == (int)RowEpi::kRHidden) {
+              o0[r] = one_minus_sq(ld(rH, vo, so)) * (v + bv);
+            } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
+              const float h = ld(rH, vo, so);
+              o0[r] = v * one_minus_sq(h);
+              o1[r] = -2.0f * v * h;
+            } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
+              o0[r] = v * one_minus_sq(ld(rH, vo, so));
+            } else {
+              o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+            st(o0[r], rO0, vo, so);
+            if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
+          }
         }
       }
+    } else {
+      // partial-width tile (odd layer widths): predicated path
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
+        const bool real = col < args.N;
+        const bool colv = col < args.Npad;
+        const int colc = colv ? col : 0;
+        float bv = 0.0f;
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden) bv = e.bias[real ? col : 0];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < M && colv) {
+              float o0, o1;
+              epi_elem_v<EPI>(e, (size_t)row * e.ldo + colc, real, acc[tm][tn][r], real ? bv : 0.0f, o0, o1);
+              epi_store<EPI>(e, (size_t)row * e.ldo + col, o0, o1);
+            }
+          }
+      }
+    }
   }
 }
 
@@ -427,23 +557,40 @@ wgrad_kernel(const WGradArgs args) {
   if (do_colsum && tid < BN && n0 + tid < args.Nb) out[args.off_b + n0 + tid] = csum;
 }
 
-template <int WM, int WN, int TM, int TN, int EPI>
+template <int WM, int WN, int TM, int TN, int BKT, int EPI>
 void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  dim3 grid((a.M + BM - 1) / BM, (a.Npad + BN - 1) / BN);
-  hipLaunchKernelGGL((rowgemm_kernel<WM, WN, TM, TN, EPI>), grid, dim3(WM * WN * 64), 0, s, a);
+  const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
+  hipLaunchKernelGGL((rowgemm_kernel<WM, WN, TM, TN, BKT, EPI>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
+                     s, a);
+}
+
+int wide_cfg() {
+  static int cfg = [] {
+    const char* e = std::getenv("TRPO_ROWCFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return cfg;
 }
 
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   if constexpr (EPI >= (int)RowEpi::kPrepHead) {
     if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
-    launch_row_cfg<4, 1, 2, 1, EPI>(a, s);
+    launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
   } else {
-    if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, EPI>(a, s);
-    else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, EPI>(a, s);
-    else if (a.Npad <= 128) launch_row_cfg<2, 2, 2, 2, EPI>(a, s);
-    else launch_row_cfg<2, 4, 2, 2, EPI>(a, s);
+    if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
+    else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
+    else if (a.Npad <= 128) launch_row_cfg<2, 2, 2, 2, 16, EPI>(a, s);
+    else {
+      switch (wide_cfg()) {
+        case 1: launch_row_cfg<2, 2, 2, 2, 16, EPI>(a, s); break;   // 128 x 128, 4 waves
+        case 2: launch_row_cfg<4, 2, 2, 2, 16, EPI>(a, s); break;   // 256 x 128, 8 waves
+        case 3: launch_row_cfg<2, 4, 2, 2, 32, EPI>(a, s); break;   // 128 x 256, BK 32
+        case 4: launch_row_cfg<1, 4, 2, 2, 16, EPI>(a, s); break;   // 64 x 256, 4 waves
+        default: launch_row_cfg<2, 4, 2, 2, 16, EPI>(a, s); break;  // 128 x 256, 8 waves
+      }
+    }
   }
 }
 
@@ -489,6 +636,219 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
     if (Mp <= 128) launch_wg_cfg<2, 4, 2, 2>(a, s);         // 128 x 256
     else launch_wg_cfg<2, 4, 4, 2>(a, s);                   // 256 x 256
   }
+}
+
+}  // namespace trpo
+
+// =============================================================================
+// Fused FVP head kernel (see kernels.h, HeadArgs)
+// =============================================================================
+namespace trpo {
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int HB_M = 64;            // rows per tile
+constexpr int HB_AMAX = 256;        // max hidden width held in LDS
+constexpr int HB_LDS_ROW = HB_AMAX + 4;
+constexpr int HB_DCAT_LD = 65;      // [RD_L | D_L] row stride (odd: conflict-free column reads)
+constexpr int HB_THREADS = 512;
+
+__device__ __forceinline__ double hsum16d(double v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+  return v;
+}
+
+__global__ void __launch_bounds__(HB_THREADS)
+fvp_head_kernel(const HeadArgs args) {
+  __shared__ __attribute__((aligned(16))) float sRH[HB_M * HB_LDS_ROW];
+  __shared__ __attribute__((aligned(16))) float sH[HB_M * HB_LDS_ROW];
+  __shared__ float sD[HB_M * HB_DCAT_LD];        // cols [0,bpad) = RD_L, [bpad,2bpad) = D_L
+  __shared__ float sRed[4 * 2 * 4 * 64];         // K-half partials of the head GEMM
+  if (args.skip && *args.skip) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int a = args.a, b = args.b, apad = args.apad, bpad = args.bpad;
+  const int split = blockIdx.x;
+  const int r0 = split * args.rows_per_split;
+  const int r1 = min(args.rows, r0 + args.rows_per_split);
+
+  // persistent weight-gradient accumulator: wave w owns hidden rows [32w, 32w+32) x cols [0,32)
+  f32x16 gacc = f32x16{};
+  float bsum = 0.0f;
+
+  for (int t0 = r0; t0 < r1; t0 += HB_M) {
+    const int nrow = min(HB_M, r1 - t0);
+    // ---- P0: stage RH, H (64 x apad) and D_L into LDS ----
+    {
+      const int q4 = apad / 4;                  // float4 per row
+      const int tot = HB_M * q4;
+      for (int f = tid; f < 2 * tot; f += HB_THREADS) {
+        const int which = f >= tot;
+        const int g = which ? f - tot : f;
+        const int r = g / q4, c4 = g % q4;
+        f32x4_t v = f32x4_t{};
+        if (r < nrow)
+          v = *reinterpret_cast<const f32x4_t*>((which ? args.H : args.RH) + (size_t)(t0 + r) * apad + 4 * c4);
+        *reinterpret_cast<f32x4_t*>((which ? sH : sRH) + r * HB_LDS_ROW + 4 * c4) = v;
+      }
+      for (int f = tid; f < HB_M * 32; f += HB_THREADS) {
+        const int r = f >> 5, c = f & 31;
+        float dl = 0.0f;
+        if (r < nrow && c < bpad) dl = args.DL[(size_t)(t0 + r) * bpad + c];
+        if (c < bpad) sD[r * HB_DCAT_LD + bpad + c] = dl;
+      }
+    }
+    __syncthreads();
+
+    // ---- P1: head GEMM RZ[64 x 32] (16x16x4 MFMA; wave = 16-row tile x K-half) ----
+    const int rt = wave & 3, kh = wave >> 2;
+    const int l15 = lane & 15, grp = lane >> 4;
+    f32x4_t hacc[2] = {f32x4_t{}, f32x4_t{}};
+    {
+      const float* sA = kh ? sH : sRH;
+      const float* W = args.WF + (size_t)kh * apad * bpad;
+      for (int kq = 0; kq < apad / 16; ++kq) {
+        const f32x4_t a4 = *reinterpret_cast<const f32x4_t*>(sA + (rt * 16 + l15) * HB_LDS_ROW + 16 * kq + 4 * grp);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = 16 * kq + 4 * grp + s;
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) {
+            const int j = 16 * tn + l15;
+            const float bv = (j < bpad) ? W[(size_t)k * bpad + j] : 0.0f;
+            hacc[tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s], bv, hacc[tn], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (kh == 1) {
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sRed[((rt * 2 + tn) * 4 + r) * 64 + lane] = hacc[tn][r];
+    }
+    __syncthreads();
+    if (kh == 0) {
+      // ---- P2: R-softmax head epilogue -> RD_L into sD[:, 0:bpad) ----
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rt * 16 + grp * 4 + r;
+        const bool rv = row < nrow;
+        double rz[2], pd[2];
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const int j = 16 * tn + l15;
+          const bool real = j < b;
+          const float z = hacc[tn][r] + sRed[((rt * 2 + tn) * 4 + r) * 64 + lane];
+          rz[tn] = real ? (double)(z + args.c[j]) : 0.0;
+          pd[tn] = (real && rv) ? (double)args.P[(size_t)(t0 + row) * bpad + j] : 0.0;
+        }
+        const double prz = hsum16d(pd[0] * rz[0] + pd[1] * rz[1]);
+        double Rp[2], Aa[2], B[2];
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const bool real = 16 * tn + l15 < b;
+          Rp[tn] = pd[tn] * (rz[tn] - prz);
+          const double den = pd[tn] + (double)kEps;
+          Aa[tn] = real ? pd[tn] / den : 0.0;
+          B[tn] = real ? (double)kEps / den : 0.0;
+        }
+        const double spB = hsum16d(pd[0] * B[0] + pd[1] * B[1]);
+        const double sRAB = hsum16d(Rp[0] * Aa[0] * B[0] + Rp[1] * Aa[1] * B[1]);
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const int j = 16 * tn + l15;
+          const double rd = args.invN * (Rp[tn] * (B[tn] - spB) + Rp[tn] * Aa[tn] * Aa[tn] + pd[tn] * sRAB);
+          if (j < bpad) sD[row * HB_DCAT_LD + j] = (j < b && rv) ? (float)rd : 0.0f;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- P3: R-backward RDH[64 x apad] = [RD_L | D_L] [W^T ; V^T] (32x32x2) + epilogue ----
+    {
+      const int lr = lane & 31, lh = lane >> 5;
+      const int rt2 = wave & 1, ct = wave >> 1;   // 2 row tiles x 4 col groups of 64
+      const int colbase = 64 * ct;
+      if (colbase < apad) {
+        f32x16 racc[2] = {f32x16{}, f32x16{}};
+        const int K = 2 * bpad;
+        for (int k0 = 0; k0 < K; k0 += 2) {
+          const int k = k0 + lh;
+          const float av = sD[(rt2 * 32 + lr) * HB_DCAT_LD + k];
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) {
+            const int col = colbase + 32 * tn + lr;
+            const float bv = col < apad ? args.WB[(size_t)k * apad + col] : 0.0f;
+            racc[tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, racc[tn], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const int col = colbase + 32 * tn + lr;
+          if (col >= apad) continue;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rt2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row >= nrow) continue;
+            const float h = sH[row * HB_LDS_ROW + col];
+            const float rh = sRH[row * HB_LDS_ROW + col];
+            const size_t gi = (size_t)(t0 + row) * apad + col;
+            const float e = args.E[gi];
+            args.RDout[gi] = (col < a) ? fmaf(e, rh, racc[tn][r] * one_minus_sq(h)) : 0.0f;
+          }
+        }
+      }
+    }
+
+    // ---- P4: weight gradient of the head: G[apad x 32] += RH^T D_L + H^T RD_L ----
+    {
+      const int lr = lane & 31, lh = lane >> 5;
+      const int i = 32 * wave + lr;          // hidden row of this lane's A fragment
+      if (32 * wave < apad) {
+        for (int rr = 0; rr < HB_M; rr += 2) {
+          const int row = rr + lh;
+          const float aRH = (i < apad) ? sRH[row * HB_LDS_ROW + i] : 0.0f;
+          const float aH = (i < apad) ? sH[row * HB_LDS_ROW + i] : 0.0f;
+          const float bD = (lr < bpad) ? sD[row * HB_DCAT_LD + bpad + lr] : 0.0f;
+          const float bR = (lr < bpad) ? sD[row * HB_DCAT_LD + lr] : 0.0f;
+          gacc = __builtin_amdgcn_mfma_f32_32x32x2f32(aRH, bD, gacc, 0, 0, 0);
+          gacc = __builtin_amdgcn_mfma_f32_32x32x2f32(aH, bR, gacc, 0, 0, 0);
+        }
+      }
+      if (tid < b) {
+        float cs = 0.0f;
+        for (int r = 0; r < HB_M; ++r) cs += sD[r * HB_DCAT_LD + tid];
+        bsum += cs;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- write this split's slab: W part (a x b) and bias ----
+  float* out = args.slab + (size_t)split * args.slab_stride;
+  {
+    const int lr = lane & 31, lh = lane >> 5;
+    const int j = lr;
+    if (32 * wave < apad && j < b) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (i < a) out[args.off_w + (int64_t)i * b + j] = gacc[r];
+      }
+    }
+  }
+  if (tid < b) out[args.off_b + tid] = bsum;
+}
+
+}  // namespace
+
+void launch_fvp_head(const HeadArgs& a, hipStream_t s) {
+  if (a.apad > HB_AMAX || a.bpad > 32) throw std::runtime_error("fvp_head: layer too wide for the fused head");
+  if (a.splits <= 0) return;
+  hipLaunchKernelGGL(fvp_head_kernel, dim3(a.splits), dim3(HB_THREADS), 0, s, a);
 }
 
 }  // namespace trpo

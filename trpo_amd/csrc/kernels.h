@@ -201,3 +201,31 @@ void launch_adv_normalize(double* adv, float* adv32, int64_t n, const double* gl
                           const double* global_sq, double inv_n, hipStream_t s);
 
 }  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Fused FVP head (gemm.hip): for the last layer (hidden width a <= 256, A <= 32)
+// one persistent kernel per split-K slab does, per 64-row tile held in LDS:
+//   RZ = RH W + H V + c ; RD_L = R-softmax-reverse(RZ)          (R-forward head)
+//   RD_{L-2} = (RD_L W^T + D_L V^T)(1-H^2) + E RH               (R-backward, hidden L-1)
+//   slab += RH^T D_L + H^T RD_L ; bias += colsum RD_L            (weight gradient, layer L-1)
+// ---------------------------------------------------------------------------
+struct HeadArgs {
+  int rows, a, b, apad, bpad;
+  const float* RH;   // [rows][apad]
+  const float* H;    // [rows][apad]
+  const float* WF;   // [2apad][bpad]  (W ; V)
+  const float* WB;   // [2bpad][apad]  (W^T ; V^T)
+  const float* c;    // [b] tangent bias
+  const float* P;    // [rows][bpad]
+  const float* DL;   // [rows][bpad]
+  const float* E;    // [rows][apad]
+  float* RDout;      // [rows][apad]
+  double invN;
+  int splits, rows_per_split;
+  float* slab;
+  int64_t slab_stride, off_w, off_b;
+  const int* skip;
+};
+void launch_fvp_head(const HeadArgs& a, hipStream_t s);
+}  // namespace trpo
