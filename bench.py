@@ -71,6 +71,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return 2 * ab
     if role == "fvp_head":          # R-forward (2ab) + R-backward (2ab) + wgrad (2ab) of the last layer
         return 3 * ab
+    if role == "fvp_headbwd":       # R-backward (2ab) + wgrad (2ab) of the last layer
+        return 2 * ab
     return 0.0
 
 

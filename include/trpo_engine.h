@@ -161,6 +161,11 @@ int trpo_device_count(int* out);
 int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, double gamma,
                   double* out, int mem);
 
+/* ---- kernel-variant switches (for A/B measurements and variant parity tests) ----------
+ * "row_cfg" (wide row-GEMM tile, 0..5), "wg_cfg" (weight-gradient tile, 0..1), "fused_head"
+ * and "head_bwd" (last-layer fusions; read when an engine is created).  Process-wide. */
+int trpo_set_option(const char* name, int value);
+
 /* ---- profiling: per-launch HIP events on the engine stream ------------------------- */
 int trpo_profile_enable(trpo_engine* e, int enable);
 /* JSON {"tag": [count, total_ms], ...}; returns bytes needed (excluding NUL) or < 0 */

@@ -265,3 +265,42 @@ def test_bad_actions_fail_loudly(gpu_available):
     with pytest.raises(EngineError, match="action"):
         e.set_batch(np.zeros((4, 4), np.float32), np.array([0, 1, 2, 0]), np.zeros(4, np.float32),
                     np.full((4, 2), .5, np.float32))
+
+
+@pytest.mark.parametrize("opts", [
+    {"fused_head": 1},                 # LDS-resident last-layer fusion (opt-in)
+    {"head_bwd": 0},                   # unfused last layer: separate R-backward and wgrad launches
+    {"row_cfg": 1}, {"row_cfg": 2}, {"row_cfg": 3}, {"row_cfg": 4}, {"row_cfg": 5},
+    {"wg_cfg": 1},
+], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_kernel_variants_parity(gpu_available, opts):
+    """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
+    C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import set_option
+    defaults = {"fused_head": 0, "head_bwd": 1, "row_cfg": 0, "wg_cfg": 0}
+    try:
+        for k, v in opts.items():
+            set_option(k, v)
+        for name in ("update_c3.npz", "update_c1.npz"):
+            d = golden(name)
+            eng, spec = make_engine(d)
+            assert_vec_close(eng.fvp(d["v"].astype(np.float32), 0.0), d["hv"], REL, f"{name} Hv {opts}")
+            assert_vec_close(eng.policy_grad(), d["g"], REL, f"{name} g {opts}")
+            st = eng.update(UpdateParams(residual_tol=float(d["residual_tol"])))
+            assert st["k"] == int(d["k"])
+            assert_vec_close(eng.get_flat(), d["theta_new"], REL, f"{name} theta {opts}")
+        # wide layers (row GEMM N = 256 path, 256x256 weight gradient)
+        spec = O.PolicySpec(128, [256, 256], 18)
+        dd = O.synthetic_batch(spec, 700, seed=21)
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=700)
+        e.set_flat(dd["theta"])
+        e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+        v = np.random.RandomState(22).standard_normal(spec.n_params).astype(np.float32)
+        ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
+        assert_vec_close(e.fvp(v, 0.0), ref, REL, f"wide Hv {opts}")
+        gref = O.policy_grad(dd["theta"].astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+        assert_vec_close(e.policy_grad(), gref, REL, f"wide g {opts}")
+    finally:
+        for k, v in defaults.items():
+            set_option(k, v)

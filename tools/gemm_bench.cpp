@@ -38,5 +38,24 @@ int main(int argc, char** argv) {
   run("tanh (2seg, no aux load)", RowEpi::kTanh, 2);
   run("rbwd (2seg, RBwd)", RowEpi::kRBwd, 2);
   run("rfwd (1seg, RHidden)", RowEpi::kRHidden, 1);
+  // weight gradient 256x256 over M rows, two segments, 512 splits
+  {
+    const int S = 512;
+    long rps = (M + S - 1) / S;
+    rps = (rps + 31) / 32 * 32;
+    float* slab = dalloc((size_t)S * (N * K + N));
+    WGradArgs w{};
+    w.rows = (int)M; w.Ma = K; w.Nb = N; w.Mpad = K; w.Npad = N; w.nseg = 2;
+    w.seg[0] = WSeg{RH, H2, K, N}; w.seg[1] = WSeg{H, E, K, N}; w.colsum_seg = 1;
+    w.splits = (int)((M + rps - 1) / rps); w.rows_per_split = (int)rps; w.slab = slab;
+    w.slab_stride = N * K + N; w.off_w = 0; w.off_b = N * K;
+    launch_wgrad(w, 0); CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) launch_wgrad(w, 0);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= reps;
+    const double fl = 2.0 * M * N * K * 2;
+    printf("%-28s M=%-9ld %8.3f ms  %6.1f TF/s\n", "wgrad (2seg 256x256)", M, ms, fl / ms / 1e9);
+  }
   return 0;
 }

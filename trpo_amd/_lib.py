@@ -68,6 +68,7 @@ SIGNATURES = {
     "trpo_update": (c_int, [c_void_p, POINTER(UpdateParams), POINTER(UpdateStats)]),
     "trpo_device_count": (c_int, [POINTER(c_int)]),
     "trpo_discount": (c_int, [c_void_p, c_void_p, c_int64, c_double, c_void_p, c_int]),
+    "trpo_set_option": (c_int, [c_char_p, c_int]),
     "trpo_profile_enable": (c_int, [c_void_p, c_int]),
     "trpo_profile_query": (c_int, [c_void_p, c_char_p, c_int]),
     "trpo_profile_reset": (c_int, [c_void_p]),
@@ -108,3 +109,8 @@ def device_count() -> int:
     n = c_int(0)
     check(lib.trpo_device_count(ctypes.byref(n)), "trpo_device_count")
     return n.value
+
+
+def set_option(name: str, value: int):
+    """Process-wide kernel-variant switch (see include/trpo_engine.h)."""
+    check(lib.trpo_set_option(name.encode(), int(value)), f"trpo_set_option({name})")

@@ -128,7 +128,8 @@ struct trpo_engine {
   UpdScalars* hsc = nullptr;   // pinned host mirror
 
   bool prepared = false;
-  bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel
+  bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
+  bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
   // profiling
   bool prof = false;
@@ -275,7 +276,8 @@ struct trpo_engine {
     fl = dalloc<CGFlags>(1);
     dbad = dalloc<int>(1);
     fused_head = L >= 2 && wp[L - 1] <= 256 && wp[L - 1] % 16 == 0 && wp[L] <= 32 &&
-                 std::getenv("TRPO_FUSED_HEAD") != nullptr;   // opt-in: slower than 3 kernels at C4 (1 block/CU)
+                 g_options.fused_head != 0;   // opt-in: slower than the split kernels at C4 (1 block/CU)
+    head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
     HIPCHECK(hipStreamSynchronize(stream));
@@ -300,7 +302,7 @@ struct trpo_engine {
     // rows per split: a multiple of the 16-row k-tile, >= 64 rows
     const int smax = S;
     int64_t rps = (n + smax - 1) / smax;
-    rps = std::max<int64_t>(64, (rps + 15) / 16 * 16);
+    rps = std::max<int64_t>(64, (rps + 31) / 32 * 32);   // multiple of the largest wgrad k-tile
     rows_per_split = (int)rps;
     active_splits = (int)std::max<int64_t>(1, (n + rps - 1) / rps);
   }
@@ -558,8 +560,37 @@ struct trpo_engine {
       launch_fvp_head(h, stream);
       check_launch();
     }
+    if (head_bwd) {
+      HeadBwdArgs h{};
+      const int l = L - 1;
+      h.rows = (int)n;
+      h.a = w[l];
+      h.b = w[l + 1];
+      h.apad = wp[l];
+      h.bpad = wp[l + 1];
+      h.RH = RH[l];
+      h.H = H[l];
+      h.E = E[l - 1];
+      h.WB = WB[l];
+      h.RDL = RD[l];
+      h.DL = D[l];
+      h.RDout = RD[l - 1];
+      h.splits = active_splits;
+      h.rows_per_split = rows_per_split;
+      h.slab = slab;
+      h.slab_stride = slab_stride;
+      h.off_w = offW[l];
+      h.off_b = offb[l];
+      h.skip = skip;
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_headbwd_l%d", l);
+      Scope sp(this, tag);
+      launch_head_bwd(h, stream);
+      check_launch();
+    }
+    const bool tail_fused = fused_head || head_bwd;
     // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
-    for (int l = fused_head ? L - 2 : L - 1; l >= 1; --l) {
+    for (int l = tail_fused ? L - 2 : L - 1; l >= 1; --l) {
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 2;
       a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
@@ -578,7 +609,7 @@ struct trpo_engine {
       check_launch();
     }
     // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
-    for (int l = 0; l < Lf; ++l) {
+    for (int l = 0; l < (tail_fused ? L - 1 : L); ++l) {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
       if (l == 0)
@@ -1109,6 +1140,18 @@ int trpo_discount(const double* x, const uint8_t* starts, int64_t n, double gamm
     (void)hipFree(ds);
     if (dx) (void)hipFree(dx);
     if (dy) (void)hipFree(dy);
+  });
+}
+
+int trpo_set_option(const char* name, int value) {
+  return guarded([&] {
+    REQUIRE(name, "NULL argument");
+    const std::string k(name);
+    if (k == "row_cfg") g_options.row_cfg = value;
+    else if (k == "wg_cfg") g_options.wg_cfg = value;
+    else if (k == "fused_head") g_options.fused_head = value;
+    else if (k == "head_bwd") g_options.head_bwd = value;
+    else throw ArgError("unknown option " + k);
   });
 }
 

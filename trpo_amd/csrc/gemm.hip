@@ -27,6 +27,13 @@
 
 namespace trpo {
 
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
+                     env_int("TRPO_HEAD_BWD", 1)};
+
 namespace {
 
 constexpr int BK = 16;
@@ -195,7 +202,7 @@ __device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
 }
 
 template <int WM, int WN, int TM, int TN, int BK, int EPI>
-__global__ void __launch_bounds__(WM* WN * 64, EPI == 2 ? 2 : 4)   // 4 waves / SIMD: <= 128 VGPRs
+__global__ void __launch_bounds__(WM* WN * 64, (TM * TN >= 8 || EPI == 2) ? 2 : 4)   // waves / SIMD
 rowgemm_kernel(const RowGemmArgs args) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int LDA = BK + 4;   // A tile [BM][BK+4]: conflict-free ds_read_b128 column groups
@@ -225,6 +232,9 @@ rowgemm_kernel(const RowGemmArgs args) {
   constexpr int AF4 = BM * BK / 4, BF4 = BK * BN / 4;
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BF4 + NT - 1) / NT;
   f32x4 ra[AP], rb[BP];
+  // validity of each staged float4; applied when the registers are written to LDS
+  // (after the compute phase), so the prefetch loads are not waited for early
+  bool oka[AP], okb[BP];
 
   auto gload = [&](int t) {
     const bool s1 = t >= nt0;
@@ -241,8 +251,8 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int row = m0 + r, k = k0 + 4 * kq;
       // branch-free guard: always load from a clamped (valid) address, select zero
       const bool ok = (AF4 % NT == 0 || f < AF4) && row < M && k < K;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
-      ra[i] = ok ? v : f32x4{};
+      ra[i] = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
+      oka[i] = ok;
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
@@ -250,8 +260,8 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int kr = f / (BN / 4), cq = f % (BN / 4);
       const int k = k0 + kr, col = n0 + 4 * cq;
       const bool ok = (BF4 % NT == 0 || f < BF4) && k < K && col < args.Npad;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? k : 0) * ldb + (ok ? col : 0));
-      rb[i] = ok ? v : f32x4{};
+      rb[i] = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? k : 0) * ldb + (ok ? col : 0));
+      okb[i] = ok;
     }
   };
   auto sstore = [&](int buf) {
@@ -262,7 +272,7 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       if (AF4 % NT == 0 || f < AF4) {
         const int r = f / (BK / 4), kq = f % (BK / 4);
-        *reinterpret_cast<f32x4*>(As + r * LDA + 4 * kq) = ra[i];
+        *reinterpret_cast<f32x4*>(As + r * LDA + 4 * kq) = oka[i] ? ra[i] : f32x4{};
       }
     }
 #pragma unroll
@@ -270,7 +280,7 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       if (BF4 % NT == 0 || f < BF4) {
         const int kr = f / (BN / 4), cq = f % (BN / 4);
-        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = rb[i];
+        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = okb[i] ? rb[i] : f32x4{};
       }
     }
   };
@@ -420,7 +430,7 @@ rowgemm_kernel(const RowGemmArgs args) {
 // ---------------------------------------------------------------------------
 // weight-gradient kernel: k = rows (split-K), tiles [BK][BM] / [BK][BN] k-major
 // ---------------------------------------------------------------------------
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int BK = 16>
 __global__ void __launch_bounds__(WM* WN * 64)
 wgrad_kernel(const WGradArgs args) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
@@ -565,13 +575,7 @@ void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
                      s, a);
 }
 
-int wide_cfg() {
-  static int cfg = [] {
-    const char* e = std::getenv("TRPO_ROWCFG");
-    return e ? std::atoi(e) : 0;
-  }();
-  return cfg;
-}
+int wide_cfg() { return g_options.row_cfg; }
 
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
@@ -588,18 +592,21 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
         case 2: launch_row_cfg<4, 2, 2, 2, 16, EPI>(a, s); break;   // 256 x 128, 8 waves
         case 3: launch_row_cfg<2, 4, 2, 2, 32, EPI>(a, s); break;   // 128 x 256, BK 32
         case 4: launch_row_cfg<1, 4, 2, 2, 16, EPI>(a, s); break;   // 64 x 256, 4 waves
+        case 5: launch_row_cfg<2, 4, 4, 2, 16, EPI>(a, s); break;   // 256 x 256, 8 waves, 128 acc/wave
         default: launch_row_cfg<2, 4, 2, 2, 16, EPI>(a, s); break;  // 128 x 256, 8 waves
       }
     }
   }
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int BKT = 16>
 void launch_wg_cfg(const WGradArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
-  hipLaunchKernelGGL((wgrad_kernel<WM, WN, TM, TN>), grid, dim3(WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((wgrad_kernel<WM, WN, TM, TN, BKT>), grid, dim3(WM * WN * 64), 0, s, a);
 }
+
+int wg_cfg() { return g_options.wg_cfg; }
 
 }  // namespace
 
@@ -634,6 +641,7 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
     else launch_wg_cfg<2, 2, 2, 2>(a, s);                   // 128 x 128
   } else {
     if (Mp <= 128) launch_wg_cfg<2, 4, 2, 2>(a, s);         // 128 x 256
+    else if (wg_cfg() == 1) launch_wg_cfg<2, 4, 4, 2, 32>(a, s);   // 256 x 256, BK 32
     else launch_wg_cfg<2, 4, 4, 2>(a, s);                   // 256 x 256
   }
 }
@@ -849,6 +857,150 @@ void launch_fvp_head(const HeadArgs& a, hipStream_t s) {
   if (a.apad > HB_AMAX || a.bpad > 32) throw std::runtime_error("fvp_head: layer too wide for the fused head");
   if (a.splits <= 0) return;
   hipLaunchKernelGGL(fvp_head_kernel, dim3(a.splits), dim3(HB_THREADS), 0, s, a);
+}
+
+}  // namespace trpo
+
+// =============================================================================
+// Fused last-layer R-backward + weight gradient (see kernels.h, HeadBwdArgs)
+// Block = 4 waves; wave w owns hidden columns [64w, 64w+64) (two 32-col MFMA
+// tiles); a tile is 32 rows.  Per tile:
+//   1. [RD_L | D_L] (32 x 2bpad) -> LDS
+//   2. RDH = [RD_L|D_L] . [W^T;V^T]   (32x32x2 MFMA, K = 2bpad; the W^T/V^T
+//      fragments of a wave never change -> held in registers for the launch)
+//   3. H, RH, E buffer-loaded in accumulator layout (lane = hidden col,
+//      register = row); RD = RDH (1-H^2) + E RH stored
+//   4. weight gradient: the same H / RH registers are the A operands of
+//      G[hidden][j] += sum_rows RH D_L + H RD_L (register r of lane half h is
+//      row (r&3)+8(r>>2)+4h, used as the MFMA k of step r)
+// =============================================================================
+namespace trpo {
+namespace {
+
+constexpr int HBW_ROWS = 32;
+constexpr int HBW_WAVES = 4;
+constexpr int HBW_DLD = 65;      // LDS row stride of [RD_L | D_L] (odd: conflict-free column reads)
+
+template <int KPAIRS>   // KPAIRS = bpad (2*bpad K values, 2 per MFMA)
+__global__ void __launch_bounds__(HBW_WAVES * 64, 2)
+head_bwd_kernel(const HeadBwdArgs args) {
+  __shared__ float sD[HBW_ROWS * HBW_DLD];
+  if (args.skip && *args.skip) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int a = args.a, b = args.b, apad = args.apad, bpad = args.bpad;
+  const int split = blockIdx.x;
+  const int r0 = split * args.rows_per_split;
+  const int r1 = min(args.rows, r0 + args.rows_per_split);
+  const int cbase = 64 * wave;                 // this wave's first hidden column
+  const bool active = cbase < apad;
+
+  // B operand of the R-backward: WB[k][cbase + 32 tn + lr] for k = 2s + lh
+  float wb[KPAIRS][2];
+#pragma unroll
+  for (int s = 0; s < KPAIRS; ++s)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int col = cbase + 32 * tn + lr;
+      const int k = 2 * s + lh;
+      wb[s][tn] = (active && col < apad && k < 2 * bpad) ? args.WB[(size_t)k * apad + col] : 0.0f;
+    }
+
+  f32x16 gacc[2] = {f32x16{}, f32x16{}};   // weight gradient, hidden rows x 32 cols
+  float bsum = 0.0f;
+
+  for (int t0 = r0; t0 < r1; t0 += HBW_ROWS) {
+    const int nrow = min(HBW_ROWS, r1 - t0);
+    // 1. [RD_L | D_L] tile
+    for (int f = tid; f < HBW_ROWS * 64; f += HBW_WAVES * 64) {
+      const int r = f >> 6, c = f & 63;
+      float v = 0.0f;
+      if (r < nrow && c < 2 * bpad) {
+        const bool second = c >= bpad;
+        const int cc = second ? c - bpad : c;
+        v = (second ? args.DL : args.RDL)[(size_t)(t0 + r) * bpad + cc];
+      }
+      if (c < 2 * bpad) sD[r * HBW_DLD + c] = v;
+    }
+    __syncthreads();
+    if (tid < b) {
+      float cs = 0.0f;
+      for (int r = 0; r < HBW_ROWS; ++r) cs += sD[r * HBW_DLD + tid];
+      bsum += cs;
+    }
+    if (active) {
+      // 2. R-backward GEMM
+      f32x16 racc[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+      for (int s = 0; s < KPAIRS; ++s) {
+        const float av = sD[lr * HBW_DLD + 2 * s + lh];
+        racc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb[s][0], racc[0], 0, 0, 0);
+        racc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb[s][1], racc[1], 0, 0, 0);
+      }
+      // 3. epilogue through per-tile buffer descriptors (rows past the tile read 0 / drop)
+      const int tile_bytes = nrow * apad * 4;
+      auto mk = [&](const float* p) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (size_t)t0 * apad), 0, tile_bytes, 0x00020000);
+      };
+      const __amdgpu_buffer_rsrc_t rH = mk(args.H), rRH = mk(args.RH), rE = mk(args.E), rO = mk(args.RDout);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        const int col = cbase + 32 * tn + lr;
+        const bool colv = col < apad;
+        const int vo = ((4 * lh) * apad + (colv ? col : 0)) * 4;
+        float h[16], rh[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int so = ((r & 3) + 8 * (r >> 2)) * apad * 4;
+          h[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rH, vo, so, 0));
+          rh[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rRH, vo, so, 0));
+          const float e = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, vo, so, 0));
+          const float rd = fmaf(e, rh[r], racc[tn][r] * one_minus_sq(h[r]));
+          if (colv) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rd), rO, vo, so, 0);
+        }
+        // 4. weight gradient: rows are the MFMA k (register r <-> row (r&3)+8(r>>2)+4h)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float dl = lr < bpad ? sD[row * HBW_DLD + bpad + lr] : 0.0f;
+          const float rdl = lr < bpad ? sD[row * HBW_DLD + lr] : 0.0f;
+          gacc[tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(rh[r], dl, gacc[tn], 0, 0, 0);
+          gacc[tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(h[r], rdl, gacc[tn], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  float* out = args.slab + (size_t)split * args.slab_stride;
+  if (active && lr < b) {
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = cbase + 32 * tn + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (i < a) out[args.off_w + (int64_t)i * b + lr] = gacc[tn][r];
+      }
+  }
+  if (tid < b) out[args.off_b + tid] = bsum;
+}
+
+}  // namespace
+
+void launch_head_bwd(const HeadBwdArgs& a, hipStream_t s) {
+  if (a.apad > 64 * HBW_WAVES || a.bpad > 32 || a.bpad % 4) throw std::runtime_error("head_bwd: unsupported layer shape");
+  if (a.splits <= 0) return;
+  const dim3 grid(a.splits), block(HBW_WAVES * 64);
+  switch (a.bpad) {
+    case 4: hipLaunchKernelGGL(head_bwd_kernel<4>, grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL(head_bwd_kernel<8>, grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL(head_bwd_kernel<12>, grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL(head_bwd_kernel<16>, grid, block, 0, s, a); break;
+    case 20: hipLaunchKernelGGL(head_bwd_kernel<20>, grid, block, 0, s, a); break;
+    case 24: hipLaunchKernelGGL(head_bwd_kernel<24>, grid, block, 0, s, a); break;
+    case 28: hipLaunchKernelGGL(head_bwd_kernel<28>, grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL(head_bwd_kernel<32>, grid, block, 0, s, a); break;
+  }
 }
 
 }  // namespace trpo

@@ -10,6 +10,16 @@
 
 namespace trpo {
 
+// Kernel-variant switches (defaults from TRPO_ROWCFG / TRPO_WGCFG / TRPO_FUSED_HEAD /
+// TRPO_HEAD_BWD; runtime-settable through trpo_set_option for A/B and parity tests).
+struct Options {
+  int row_cfg;     // wide row-GEMM tile: 0 = 128x256 (8 waves), 1 = 128x128, 2 = 256x128, 3 = BK32, 4 = 64x256, 5 = 256x256
+  int wg_cfg;      // 256x256 weight-gradient tile: 0 = BK16, 1 = BK32
+  int fused_head;  // engine: last-layer R-fwd + R-bwd + wgrad in one LDS-resident kernel
+  int head_bwd;    // engine: last-layer R-bwd + wgrad in one kernel
+};
+extern Options g_options;
+
 // ---------------------------------------------------------------------------
 // Row GEMM:  C[M x N] = sum_seg A_seg[M x K_seg] * B_seg[K_seg x Npad]  -> epilogue
 // ---------------------------------------------------------------------------
@@ -228,4 +238,29 @@ struct HeadArgs {
   const int* skip;
 };
 void launch_fvp_head(const HeadArgs& a, hipStream_t s);
+}  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Fused last-layer R-backward + weight gradient (gemm.hip), persistent per split:
+//   RD_{L-2} = ([RD_L | D_L] [W^T ; V^T]) (1 - H^2) + E RH       (hidden L-1, width a)
+//   slab    += RH^T D_L + H^T RD_L ;  bias += colsum RD_L          (layer L-1, a x b)
+// H / RH / E are read once, in MFMA accumulator layout, and reused as the A
+// operands of the weight-gradient MFMAs (rows as the K dimension).
+// ---------------------------------------------------------------------------
+struct HeadBwdArgs {
+  int rows, a, b, apad, bpad;
+  const float* RH;   // [rows][apad]
+  const float* H;    // [rows][apad]
+  const float* E;    // [rows][apad]
+  const float* WB;   // [2bpad][apad]  (W^T ; V^T)
+  const float* RDL;  // [rows][bpad]
+  const float* DL;   // [rows][bpad]
+  float* RDout;      // [rows][apad]
+  int splits, rows_per_split;
+  float* slab;
+  int64_t slab_stride, off_w, off_b;
+  const int* skip;
+};
+void launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 }  // namespace trpo
