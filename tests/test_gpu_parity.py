@@ -269,7 +269,8 @@ def test_bad_actions_fail_loudly(gpu_available):
 
 @pytest.mark.parametrize("opts", [
     {"fused_head": 1},                 # LDS-resident last-layer fusion (opt-in)
-    {"head_bwd": 0},                   # unfused last layer: separate R-backward and wgrad launches
+    {"head_bwd": 1},                   # last-layer R-backward + wgrad in one kernel (opt-in)
+    {"narrow_pf": 2},                  # two-stage prefetch for the narrow memory-bound tiles
     {"row_cfg": 1}, {"row_cfg": 2}, {"row_cfg": 3}, {"row_cfg": 4}, {"row_cfg": 5},
     {"wg_cfg": 1},
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -278,7 +279,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import set_option
-    defaults = {"fused_head": 0, "head_bwd": 1, "row_cfg": 0, "wg_cfg": 0}
+    defaults = {"fused_head": 0, "head_bwd": 0, "row_cfg": 0, "wg_cfg": 0, "narrow_pf": 1}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -304,3 +305,25 @@ def test_kernel_variants_parity(gpu_available, opts):
     finally:
         for k, v in defaults.items():
             set_option(k, v)
+
+
+def test_two_ranks_share_gpu_host_allreduce(gpu_available):
+    """Two processes, one GPU: the engine's whole multi-rank sequence (path-aligned shards,
+    1/N_global partials, all-reduced FVP / gradient / losses / standardisation sums, replicated
+    CG) with the all-reduce carried by gloo; ranks must end bitwise identical and equal a
+    single-rank engine."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tools", "mrank_check.py"),
+           "--host-allreduce"]
+    res = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
+    assert "MRANK OK" in res.stdout

@@ -26,7 +26,14 @@ def main():
     d = O.synthetic_batch(spec, n, seed=3, episode_len=200)
     lo, hi = shard_bounds(n, world, d["starts"])[rank]
     e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=hi - lo, device=dev)
-    init_engine_comm(e, rank, world)
+    if "--host-allreduce" in sys.argv:
+        # ranks share a GPU (RCCL refuses duplicate devices): all-reduce through gloo on the host
+        def ar(arr):
+            t = torch.from_numpy(arr)
+            dist.all_reduce(t)
+        e.comm_set_host_allreduce(ar, rank, world)
+    else:
+        init_engine_comm(e, rank, world)
     e.set_flat(d["theta"])
     e.set_batch(d["X"][lo:hi], d["actions"][lo:hi], None, d["old_dist"][lo:hi], n_global=n)
     e.set_rewards(d["rewards"][lo:hi], d["starts"][lo:hi])

@@ -37,6 +37,7 @@ class UpdateStats(ctypes.Structure):
 
 
 FAX_CB = CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p)
+ALLREDUCE_CB = CFUNCTYPE(c_int, c_void_p, c_int64, c_int, c_void_p)
 F32, F64 = 0, 1
 
 # name -> (restype, argtypes); every symbol include/trpo_engine.h declares
@@ -49,6 +50,7 @@ SIGNATURES = {
     "trpo_stream": (c_void_p, [c_void_p]),
     "trpo_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "trpo_comm_init": (c_int, [c_void_p, POINTER(c_uint8), c_int, c_int]),
+    "trpo_comm_set_host_allreduce": (c_int, [c_void_p, ALLREDUCE_CB, c_void_p, c_int, c_int]),
     "trpo_set_flat": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_get_flat": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_get_vector": (c_int, [c_void_p, c_int, c_void_p, c_int]),

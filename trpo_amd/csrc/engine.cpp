@@ -100,6 +100,9 @@ struct trpo_engine {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  trpo_allreduce_cb host_ar = nullptr;   // test transport (trpo_comm_set_host_allreduce)
+  void* host_ar_ctx = nullptr;
+  std::vector<uint8_t> host_ar_buf;
 
   // ---- device buffers ----
   std::vector<void*> allocs;
@@ -323,13 +326,23 @@ struct trpo_engine {
     HIPCHECK(hipStreamSynchronize(stream));
   }
 
+  void host_allreduce(void* buf, size_t bytes, size_t count, int dtype) {
+    host_ar_buf.resize(bytes);
+    HIPCHECK(hipMemcpyAsync(host_ar_buf.data(), buf, bytes, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    REQUIRE(host_ar(host_ar_buf.data(), (int64_t)count, dtype, host_ar_ctx) == 0, "host all-reduce callback failed");
+    HIPCHECK(hipMemcpyAsync(buf, host_ar_buf.data(), bytes, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
   void allreduce_f32(float* buf, size_t count) {
     if (world <= 1) return;
     Scope sp(this, "allreduce");
+    if (host_ar) return host_allreduce(buf, count * sizeof(float), count, TRPO_F32);
     NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, stream));
   }
   void allreduce_f64(double* buf, size_t count) {
     if (world <= 1) return;
+    if (host_ar) return host_allreduce(buf, count * sizeof(double), count, TRPO_F64);
     NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream));
   }
 
@@ -793,6 +806,17 @@ int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world) {
   });
 }
 
+int trpo_comm_set_host_allreduce(trpo_engine* e, trpo_allreduce_cb cb, void* ctx, int rank, int world) {
+  return guarded([&] {
+    REQUIRE(e && cb, "NULL argument");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    e->host_ar = cb;
+    e->host_ar_ctx = ctx;
+    e->rank = rank;
+    e->world = world;
+  });
+}
+
 int trpo_set_flat(trpo_engine* e, const float* theta, int mem) {
   return guarded([&] {
     REQUIRE(e && theta, "NULL argument");
@@ -1151,6 +1175,7 @@ int trpo_set_option(const char* name, int value) {
     else if (k == "wg_cfg") g_options.wg_cfg = value;
     else if (k == "fused_head") g_options.fused_head = value;
     else if (k == "head_bwd") g_options.head_bwd = value;
+    else if (k == "narrow_pf") g_options.narrow_pf = value;
     else throw ArgError("unknown option " + k);
   });
 }

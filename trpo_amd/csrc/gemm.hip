@@ -32,7 +32,7 @@ static int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
-                     env_int("TRPO_HEAD_BWD", 1)};
+                     env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1)};
 
 namespace {
 
@@ -201,7 +201,7 @@ __device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
   nt = swz - mt * ntn;
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int EPI>
+template <int WM, int WN, int TM, int TN, int BK, int EPI, int PF = 1>
 __global__ void __launch_bounds__(WM* WN * 64, (TM * TN >= 8 || EPI == 2) ? 2 : 4)   // waves / SIMD
 rowgemm_kernel(const RowGemmArgs args) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
@@ -231,12 +231,15 @@ rowgemm_kernel(const RowGemmArgs args) {
 
   constexpr int AF4 = BM * BK / 4, BF4 = BK * BN / 4;
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BF4 + NT - 1) / NT;
-  f32x4 ra[AP], rb[BP];
-  // validity of each staged float4; applied when the registers are written to LDS
-  // (after the compute phase), so the prefetch loads are not waited for early
-  bool oka[AP], okb[BP];
+  // One register stage of a k-tile.  The validity of each staged float4 is applied
+  // when the registers are written to LDS (after the compute phase), so the prefetch
+  // loads are not waited for early.  PF = 2 keeps two stages in flight.
+  struct Stage {
+    f32x4 ra[AP], rb[BP];
+    bool oka[AP], okb[BP];
+  };
 
-  auto gload = [&](int t) {
+  auto gload = [&](Stage& st, int t) {
     const bool s1 = t >= nt0;
     const float* Ap = s1 ? args.seg[1].A : args.seg[0].A;
     const float* Bp = s1 ? args.seg[1].B : args.seg[0].B;
@@ -251,8 +254,8 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int row = m0 + r, k = k0 + 4 * kq;
       // branch-free guard: always load from a clamped (valid) address, select zero
       const bool ok = (AF4 % NT == 0 || f < AF4) && row < M && k < K;
-      ra[i] = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
-      oka[i] = ok;
+      st.ra[i] = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
+      st.oka[i] = ok;
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
@@ -260,11 +263,11 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int kr = f / (BN / 4), cq = f % (BN / 4);
       const int k = k0 + kr, col = n0 + 4 * cq;
       const bool ok = (BF4 % NT == 0 || f < BF4) && k < K && col < args.Npad;
-      rb[i] = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? k : 0) * ldb + (ok ? col : 0));
-      okb[i] = ok;
+      st.rb[i] = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? k : 0) * ldb + (ok ? col : 0));
+      st.okb[i] = ok;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](const Stage& st, int buf) {
     float* As = smem + buf * (ASZ + BSZ);
     float* Bs = As + ASZ;
 #pragma unroll
@@ -272,7 +275,7 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       if (AF4 % NT == 0 || f < AF4) {
         const int r = f / (BK / 4), kq = f % (BK / 4);
-        *reinterpret_cast<f32x4*>(As + r * LDA + 4 * kq) = oka[i] ? ra[i] : f32x4{};
+        *reinterpret_cast<f32x4*>(As + r * LDA + 4 * kq) = st.oka[i] ? st.ra[i] : f32x4{};
       }
     }
 #pragma unroll
@@ -280,7 +283,7 @@ rowgemm_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       if (BF4 % NT == 0 || f < BF4) {
         const int kr = f / (BN / 4), cq = f % (BN / 4);
-        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = okb[i] ? rb[i] : f32x4{};
+        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = st.okb[i] ? st.rb[i] : f32x4{};
       }
     }
   };
@@ -310,14 +313,37 @@ rowgemm_kernel(const RowGemmArgs args) {
   };
 
   if (ntiles > 0) {
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-      if (t + 1 < ntiles) gload(t + 1);
-      compute(t & 1);
-      if (t + 1 < ntiles) sstore((t + 1) & 1);
+    if constexpr (PF == 1) {
+      Stage S;
+      gload(S, 0);
+      sstore(S, 0);
       __syncthreads();
+      for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(S, t + 1);
+        compute(t & 1);
+        if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
+        __syncthreads();
+      }
+    } else {
+      // two stages in flight: tile t in LDS buffer t&1, tile t+1 in a register stage,
+      // tile t+2 being loaded; unrolled by two so each stage has a static name
+      Stage S0, S1;
+      gload(S0, 0);
+      if (1 < ntiles) gload(S1, 1);
+      sstore(S0, 0);
+      __syncthreads();
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        if (t + 2 < ntiles) gload(S0, t + 2);
+        compute(0);
+        sstore(S1, 1);
+        __syncthreads();
+        if (t + 3 < ntiles) gload(S1, t + 3);
+        compute(1);
+        if (t + 2 < ntiles) sstore(S0, 0);
+        __syncthreads();
+      }
+      if (t < ntiles) compute(0);
     }
   }
 
@@ -430,7 +456,7 @@ rowgemm_kernel(const RowGemmArgs args) {
 // ---------------------------------------------------------------------------
 // weight-gradient kernel: k = rows (split-K), tiles [BK][BM] / [BK][BN] k-major
 // ---------------------------------------------------------------------------
-template <int WM, int WN, int TM, int TN, int BK = 16>
+template <int WM, int WN, int TM, int TN, int BK = 16, int PF = 1>
 __global__ void __launch_bounds__(WM* WN * 64)
 wgrad_kernel(const WGradArgs args) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
@@ -458,9 +484,12 @@ wgrad_kernel(const WGradArgs args) {
 
   constexpr int AF4 = BK * BM / 4, BF4 = BK * BN / 4;
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BF4 + NT - 1) / NT;
-  f32x4 ra[AP], rb[BP];
+  struct Stage {   // masks applied at the LDS store, after compute (keeps the prefetch in flight)
+    f32x4 ra[AP], rb[BP];
+    bool oka[AP], okb[BP];
+  };
 
-  auto gload = [&](int t) {
+  auto gload = [&](Stage& st, int t) {
     const int sg = t / nk;
     const int kt = t - sg * nk;
     const float* Ap = sg ? args.seg[1].A : args.seg[0].A;
@@ -473,23 +502,23 @@ wgrad_kernel(const WGradArgs args) {
       const int f = tid + i * NT;
       const int kr = f / (BM / 4), cq = f % (BM / 4);
       const int r = rb0 + kr, c = m0 + 4 * cq;
-      f32x4 v = f32x4{};
-      if ((AF4 % NT == 0 || f < AF4) && r < r1 && c < args.Mpad)
-        v = *reinterpret_cast<const f32x4*>(Ap + (size_t)r * lda + c);
-      ra[i] = v;
+      const bool ok = (AF4 % NT == 0 || f < AF4) && r < r1 && c < args.Mpad;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? r : r0) * lda + (ok ? c : 0));
+      st.ra[i] = v;
+      st.oka[i] = ok;
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
       const int f = tid + i * NT;
       const int kr = f / (BN / 4), cq = f % (BN / 4);
       const int r = rb0 + kr, c = n0 + 4 * cq;
-      f32x4 v = f32x4{};
-      if ((BF4 % NT == 0 || f < BF4) && r < r1 && c < args.Npad)
-        v = *reinterpret_cast<const f32x4*>(Bp + (size_t)r * ldb + c);
-      rb[i] = v;
+      const bool ok = (BF4 % NT == 0 || f < BF4) && r < r1 && c < args.Npad;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Bp + (size_t)(ok ? r : r0) * ldb + (ok ? c : 0));
+      st.rb[i] = v;
+      st.okb[i] = ok;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](const Stage& st, int buf) {
     float* As = smem + buf * (ASZ + BSZ);
     float* Bs = As + ASZ;
 #pragma unroll
@@ -497,7 +526,7 @@ wgrad_kernel(const WGradArgs args) {
       const int f = tid + i * NT;
       if (AF4 % NT == 0 || f < AF4) {
         const int kr = f / (BM / 4), cq = f % (BM / 4);
-        *reinterpret_cast<f32x4*>(As + kr * LDA + 4 * cq) = ra[i];
+        *reinterpret_cast<f32x4*>(As + kr * LDA + 4 * cq) = st.oka[i] ? st.ra[i] : f32x4{};
       }
     }
 #pragma unroll
@@ -505,7 +534,7 @@ wgrad_kernel(const WGradArgs args) {
       const int f = tid + i * NT;
       if (BF4 % NT == 0 || f < BF4) {
         const int kr = f / (BN / 4), cq = f % (BN / 4);
-        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = rb[i];
+        *reinterpret_cast<f32x4*>(Bs + kr * LDB + 4 * cq) = st.okb[i] ? st.rb[i] : f32x4{};
       }
     }
   };
@@ -539,15 +568,37 @@ wgrad_kernel(const WGradArgs args) {
     }
   };
 
+  auto cs_of = [&](int t) { return do_colsum && (t / nk) == args.colsum_seg; };
   if (ntiles > 0) {
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-      if (t + 1 < ntiles) gload(t + 1);
-      compute(t & 1, do_colsum && (t / nk) == args.colsum_seg);
-      if (t + 1 < ntiles) sstore((t + 1) & 1);
+    if constexpr (PF == 1) {
+      Stage S;
+      gload(S, 0);
+      sstore(S, 0);
       __syncthreads();
+      for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(S, t + 1);
+        compute(t & 1, cs_of(t));
+        if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
+        __syncthreads();
+      }
+    } else {
+      Stage S0, S1;
+      gload(S0, 0);
+      if (1 < ntiles) gload(S1, 1);
+      sstore(S0, 0);
+      __syncthreads();
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        if (t + 2 < ntiles) gload(S0, t + 2);
+        compute(0, cs_of(t));
+        sstore(S1, 1);
+        __syncthreads();
+        if (t + 3 < ntiles) gload(S1, t + 3);
+        compute(1, cs_of(t + 1));
+        if (t + 2 < ntiles) sstore(S0, 0);
+        __syncthreads();
+      }
+      if (t < ntiles) compute(0, cs_of(t));
     }
   }
 
@@ -567,12 +618,12 @@ wgrad_kernel(const WGradArgs args) {
   if (do_colsum && tid < BN && n0 + tid < args.Nb) out[args.off_b + n0 + tid] = csum;
 }
 
-template <int WM, int WN, int TM, int TN, int BKT, int EPI>
+template <int WM, int WN, int TM, int TN, int BKT, int EPI, int PF = 1>
 void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
-  hipLaunchKernelGGL((rowgemm_kernel<WM, WN, TM, TN, BKT, EPI>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
-                     s, a);
+  hipLaunchKernelGGL((rowgemm_kernel<WM, WN, TM, TN, BKT, EPI, PF>), dim3((unsigned)nblk), dim3(WM * WN * 64),
+                     0, s, a);
 }
 
 int wide_cfg() { return g_options.row_cfg; }
@@ -581,7 +632,8 @@ template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   if constexpr (EPI >= (int)RowEpi::kPrepHead) {
     if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
-    launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
+    if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
+    else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
   } else {
     if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
     else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
@@ -599,11 +651,11 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   }
 }
 
-template <int WM, int WN, int TM, int TN, int BKT = 16>
+template <int WM, int WN, int TM, int TN, int BKT = 16, int PF = 1>
 void launch_wg_cfg(const WGradArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
-  hipLaunchKernelGGL((wgrad_kernel<WM, WN, TM, TN, BKT>), grid, dim3(WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((wgrad_kernel<WM, WN, TM, TN, BKT, PF>), grid, dim3(WM * WN * 64), 0, s, a);
 }
 
 int wg_cfg() { return g_options.wg_cfg; }
@@ -640,7 +692,10 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
     if (Mp <= 64) launch_wg_cfg<1, 2, 2, 2>(a, s);          // 64 x 128
     else launch_wg_cfg<2, 2, 2, 2>(a, s);                   // 128 x 128
   } else {
-    if (Mp <= 128) launch_wg_cfg<2, 4, 2, 2>(a, s);         // 128 x 256
+    if (Mp <= 128) {
+      if (g_options.narrow_pf == 2) launch_wg_cfg<2, 4, 2, 2, 16, 2>(a, s);   // 128 x 256, 2 stages
+      else launch_wg_cfg<2, 4, 2, 2>(a, s);                                 // 128 x 256
+    }
     else if (wg_cfg() == 1) launch_wg_cfg<2, 4, 4, 2, 32>(a, s);   // 256 x 256, BK 32
     else launch_wg_cfg<2, 4, 4, 2>(a, s);                   // 256 x 256
   }

@@ -17,6 +17,7 @@ struct Options {
   int wg_cfg;      // 256x256 weight-gradient tile: 0 = BK16, 1 = BK32
   int fused_head;  // engine: last-layer R-fwd + R-bwd + wgrad in one LDS-resident kernel
   int head_bwd;    // engine: last-layer R-bwd + wgrad in one kernel
+  int narrow_pf;   // prefetch depth (1 or 2) of the memory-bound narrow tiles (softmax head, 128x256 wgrad)
 };
 extern Options g_options;
 

@@ -129,6 +129,20 @@ class Engine:
         buf = (ctypes.c_uint8 * 128)(*uid)
         check(lib.trpo_comm_init(self._h, buf, int(rank), int(world)), "trpo_comm_init")
 
+    def comm_set_host_allreduce(self, fn, rank: int, world: int):
+        """Test transport: fn(numpy_array) must sum the array across ranks in place."""
+        def cb(ptr, count, dtype, _ctx):
+            try:
+                ct = ctypes.c_double if dtype == _lib.F64 else ctypes.c_float
+                arr = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(count,))
+                fn(arr)
+                return 0
+            except Exception:   # pragma: no cover
+                return 1
+        self._host_ar = _lib.ALLREDUCE_CB(cb)   # keep alive
+        check(lib.trpo_comm_set_host_allreduce(self._h, self._host_ar, None, int(rank), int(world)),
+              "trpo_comm_set_host_allreduce")
+
     # ------------------------------------------------------------------ params
     def _out(self, out, dtype, n):
         if out is None:
