@@ -167,9 +167,13 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
                   double* out, int mem);
 
 /* ---- kernel-variant switches (for A/B measurements and variant parity tests) ----------
- * "row_cfg" (wide row-GEMM tile, 0..5), "wg_cfg" (weight-gradient tile, 0..1), "fused_head"
- * and "head_bwd" (last-layer fusions; read when an engine is created).  Process-wide. */
+ * "row_cfg" (wide f32 row-GEMM tile, 0..5), "wg_cfg" (weight-gradient tile, 0..1),
+ * "narrow_pf" (prefetch depth of the narrow tiles, 1..2), "split_mfma" (0 = f32 MFMA row GEMMs;
+ * 1..7 = split-bf16 row-GEMM tile for outputs wider than 128), "split_wg" (0 = f32 weight
+ * gradients; 1..3 = split-bf16 tile for fan_out > 128), "fused_head" and "head_bwd"
+ * (last-layer fusions; read when an engine is created).  Process-wide. */
 int trpo_set_option(const char* name, int value);
+int trpo_get_option(const char* name, int* value);
 
 /* ---- profiling: per-launch HIP events on the engine stream ------------------------- */
 int trpo_profile_enable(trpo_engine* e, int enable);

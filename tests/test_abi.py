@@ -62,3 +62,16 @@ def test_errors_are_reported_not_crashes():
     rc = _lib.lib.trpo_create(ctypes.byref(h), 4, (ctypes.c_int * 1)(64), 1, 40, 100, 0)   # A > 32
     assert rc != 0
     assert b"n_actions" in _lib.lib.trpo_last_error()
+
+
+def test_option_roundtrip():
+    """Kernel-variant switches are readable and writable without a GPU; unknown names fail."""
+    from trpo_amd._lib import EngineError, get_option, set_option
+    old = get_option("split_mfma")
+    try:
+        set_option("split_mfma", 5)
+        assert get_option("split_mfma") == 5
+    finally:
+        set_option("split_mfma", old)
+    with pytest.raises(EngineError, match="unknown option"):
+        set_option("no_such_option", 1)

@@ -273,13 +273,18 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"narrow_pf": 2},                  # two-stage prefetch for the narrow memory-bound tiles
     {"row_cfg": 1}, {"row_cfg": 2}, {"row_cfg": 3}, {"row_cfg": 4}, {"row_cfg": 5},
     {"wg_cfg": 1},
+    {"split_mfma": 0}, {"split_mfma": 1}, {"split_mfma": 2}, {"split_mfma": 3}, {"split_mfma": 4},
+    {"split_mfma": 5}, {"split_mfma": 6}, {"split_mfma": 7},
+    {"split_wg": 0}, {"split_wg": 1}, {"split_wg": 2}, {"split_wg": 3},
+    {"split_mfma": 5, "split_wg": 1},
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
     C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles."""
     from trpo_amd import Engine, UpdateParams
-    from trpo_amd._lib import set_option
-    defaults = {"fused_head": 0, "head_bwd": 0, "row_cfg": 0, "wg_cfg": 0, "narrow_pf": 1}
+    from trpo_amd._lib import get_option, set_option
+    defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
+                                           "split_wg")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -302,6 +307,22 @@ def test_kernel_variants_parity(gpu_available, opts):
         assert_vec_close(e.fvp(v, 0.0), ref, REL, f"wide Hv {opts}")
         gref = O.policy_grad(dd["theta"].astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
         assert_vec_close(e.policy_grad(), gref, REL, f"wide g {opts}")
+        # odd wide widths: K not a multiple of 16, a partial 256-column tile, 3 hidden layers
+        spec = O.PolicySpec(37, [200, 264, 144], 5)
+        dd = O.synthetic_batch(spec, 1337, seed=23)
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=1337)
+        e.set_flat(dd["theta"])
+        e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+        v = np.random.RandomState(24).standard_normal(spec.n_params).astype(np.float32)
+        ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
+        assert_vec_close(e.fvp(v, 0.0), ref, REL, f"odd-wide Hv {opts}")
+        gref = O.policy_grad(dd["theta"].astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+        assert_vec_close(e.policy_grad(), gref, REL, f"odd-wide g {opts}")
+        st = e.update(UpdateParams(residual_tol=0.0))
+        r = O.trpo_update(dd["theta"].astype(np.float64), O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]),
+                          spec, np.float64, 10, 0.0)
+        assert st["k"] == r.k
+        assert_vec_close(e.get_flat(), r.theta_new, REL, f"odd-wide theta {opts}")
     finally:
         for k, v in defaults.items():
             set_option(k, v)

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (CFUNCTYPE, POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint8,
+from ctypes import (CFUNCTYPE, POINTER, byref, c_char_p, c_double, c_float, c_int, c_int64, c_uint8,
                     c_void_p)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +71,7 @@ SIGNATURES = {
     "trpo_device_count": (c_int, [POINTER(c_int)]),
     "trpo_discount": (c_int, [c_void_p, c_void_p, c_int64, c_double, c_void_p, c_int]),
     "trpo_set_option": (c_int, [c_char_p, c_int]),
+    "trpo_get_option": (c_int, [c_char_p, POINTER(c_int)]),
     "trpo_profile_enable": (c_int, [c_void_p, c_int]),
     "trpo_profile_query": (c_int, [c_void_p, c_char_p, c_int]),
     "trpo_profile_reset": (c_int, [c_void_p]),
@@ -116,3 +117,9 @@ def device_count() -> int:
 def set_option(name: str, value: int):
     """Process-wide kernel-variant switch (see include/trpo_engine.h)."""
     check(lib.trpo_set_option(name.encode(), int(value)), f"trpo_set_option({name})")
+
+
+def get_option(name: str) -> int:
+    out = c_int(0)
+    check(lib.trpo_get_option(name.encode(), byref(out)), f"trpo_get_option({name})")
+    return out.value

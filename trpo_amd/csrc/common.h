@@ -46,4 +46,10 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n, do
   return block_sum_d(v, scratch);
 }
 
+
+// Workgroup barrier for an LDS hand-off only: waits for this wave's LDS operations,
+// not for its outstanding global loads.  __syncthreads() also emits vmcnt(0), which
+// would drain a register prefetch that is meant to stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 }  // namespace trpo

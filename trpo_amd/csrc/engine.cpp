@@ -111,6 +111,10 @@ struct trpo_engine {
   float *hv = nullptr, *stepdir = nullptr, *fullstep = nullptr, *vin = nullptr, *vout = nullptr;
   std::vector<float*> WF, WB, WFt;   // packed [W;V], [W^T;V^T], trial forward weights
   float* WBt_scratch = nullptr;
+  // bf16 (hi, mid, lo) planes of the packed matrices for the split-bf16 row GEMM:
+  // [part][3][Npad][r16(K)], part 0 = W half, 1 = V half (WF3t: W half only)
+  std::vector<uint16_t*> WF3, WB3, WFt3;
+  bool w3_valid = false;   // W halves of WF3/WB3 match WF/WB
   float* X = nullptr;
   int* act = nullptr;
   float *adv32 = nullptr, *old = nullptr;
@@ -235,6 +239,11 @@ struct trpo_engine {
       maxpad = std::max<int>(maxpad, 2 * wp[l] * wp[l + 1]);
     }
     WBt_scratch = dalloc<float>(maxpad);
+    for (int l = 0; l < L; ++l) {
+      WF3.push_back(dalloc<uint16_t>(2 * plane3_f(l) * 3));
+      WB3.push_back(dalloc<uint16_t>(2 * plane3_b(l) * 3));
+      WFt3.push_back(dalloc<uint16_t>(plane3_f(l) * 3));
+    }
     X = dalloc<float>((size_t)cap * wp[0]);
     act = dalloc<int>(cap);
     adv32 = dalloc<float>(cap);
@@ -362,6 +371,52 @@ struct trpo_engine {
     return pa;
   }
 
+  // ---- split-bf16 planes ----
+  static int r16(int k) { return (k + 15) / 16 * 16; }
+  size_t plane3_f(int l) const { return (size_t)wp[l + 1] * r16(wp[l]); }   // WF part: K = wp[l], N = wp[l+1]
+  size_t plane3_b(int l) const { return (size_t)wp[l] * r16(wp[l + 1]); }   // WB part: K = wp[l+1], N = wp[l]
+  SplitJob job_f(const std::vector<float*>& wf, const std::vector<uint16_t*>& wf3, int l, int part) const {
+    return SplitJob{wf[l] + (size_t)part * wp[l] * wp[l + 1], wf3[l] + part * 3 * plane3_f(l), wp[l], wp[l + 1],
+                    wp[l + 1], r16(wp[l])};
+  }
+  SplitJob job_b(int l, int part) const {
+    return SplitJob{WB[l] + (size_t)part * wp[l + 1] * wp[l], WB3[l] + part * 3 * plane3_b(l), wp[l + 1], wp[l],
+                    wp[l], r16(wp[l + 1])};
+  }
+  // attach the planes of a packed matrix part to a row-GEMM segment
+  static void seg3(GemmSeg& sg, uint16_t* base, size_t plane, int part, int K) {
+    sg.B3 = base + part * 3 * plane;
+    sg.ldk = r16(K);
+    sg.plane = (int)plane;
+  }
+  bool split_on() const { return g_options.split_mfma != 0; }
+  // split the given packed-matrix parts; only layers whose GEMM takes the split path
+  void split_parts(bool fwd_w, bool fwd_v, bool bwd_w, bool bwd_v, const std::vector<float*>& wf,
+                   const std::vector<uint16_t*>& wf3, const int* skip, const char* tag) {
+    if (!split_on()) return;
+    SplitArgs sa{};
+    for (int l = 0; l < L; ++l) {
+      const bool f = rowgemm_uses_split(wp[l + 1], RowEpi::kTanh);   // layer l's forward output
+      const bool b = l >= 1 && rowgemm_uses_split(wp[l], RowEpi::kRBwd);   // backward into layer l's input
+      if (f && fwd_w) sa.job[sa.n++] = job_f(wf, wf3, l, 0);
+      if (f && fwd_v) sa.job[sa.n++] = job_f(wf, wf3, l, 1);
+      if (b && bwd_w) sa.job[sa.n++] = job_b(l, 0);
+      if (b && bwd_v) sa.job[sa.n++] = job_b(l, 1);
+      if (sa.n > kMaxSplitJobs - 4 || (l == L - 1 && sa.n)) {
+        Scope sp(this, tag);
+        launch_split_b(sa, skip, stream);
+        sa.n = 0;
+      }
+    }
+    check_launch();
+  }
+  void ensure_w3() {
+    if (split_on() && !w3_valid) {
+      split_parts(true, false, true, false, WF, WF3, nullptr, "split_w");
+      w3_valid = true;
+    }
+  }
+
   RowGemmArgs row_args(int l_out_width, int l_out_pad) {
     RowGemmArgs a{};
     a.M = (int)n;
@@ -372,12 +427,13 @@ struct trpo_engine {
 
   // forward through layers 0..L-1 with weights packed in wf (W half); the head
   // epilogue is `head`; hidden activations go to `hout`
-  void forward(const std::vector<float*>& wf, const float* th, const std::vector<float*>& hout,
-               RowEpi head, const char* tag) {
+  void forward(const std::vector<float*>& wf, const std::vector<uint16_t*>& wf3, const float* th,
+               const std::vector<float*>& hout, RowEpi head, const char* tag) {
     for (int l = 0; l < L; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{l == 0 ? X : hout[l], wf[l], wp[l], wp[l + 1], wp[l]};
+      seg3(a.seg[0], wf3[l], plane3_f(l), 0, wp[l]);
       a.ea.bias = th + offb[l];
       a.ea.ldo = wp[l + 1];
       if (l < L - 1) {
@@ -419,12 +475,15 @@ struct trpo_engine {
     if (prepared) return;
     PackArgs pa = pack_args(WF, &WB);
     launch_pack(pa, theta, 0, nullptr, stream);
-    forward(WF, theta, H, RowEpi::kPrepHead, "fwd");
+    w3_valid = false;
+    ensure_w3();
+    forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
     // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H
     for (int l = L - 1; l >= 1; --l) {
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{D[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+      seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
       a.epi = RowEpi::kPrepBwd;
       a.ea.H = H[l];
       a.ea.out0 = D[l - 1];
@@ -476,6 +535,7 @@ struct trpo_engine {
   // flatgrad(surr) (trpo_inksci.py:54) -> g (all ranks)
   void policy_grad() {
     prepare();
+    ensure_w3();
     // surr backward: DS_{l-1} = (DS_l W_l^T)(1-H_l^2) ; DS of hidden layers lives in RD scratch
     std::vector<float*> DS(L);
     DS[L - 1] = DSL;
@@ -484,6 +544,7 @@ struct trpo_engine {
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{DS[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+      seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
       a.epi = RowEpi::kPgBwd;
       a.ea.H = H[l];
       a.ea.out0 = DS[l - 1];
@@ -510,6 +571,8 @@ struct trpo_engine {
       launch_pack(pa, v, 1, skip, stream);
       check_launch();
     }
+    ensure_w3();
+    split_parts(false, true, false, true, WF, WF3, skip, "split_v");
     // R-forward
     const int Lf = fused_head ? L - 1 : L;
     for (int l = 0; l < Lf; ++l) {
@@ -518,10 +581,13 @@ struct trpo_engine {
       if (l == 0) {
         a.nseg = 1;
         a.seg[0] = GemmSeg{X, Vpart, wp[0], wp[1], wp[0]};
+        seg3(a.seg[0], WF3[l], plane3_f(l), 1, wp[l]);
       } else {
         a.nseg = 2;
         a.seg[0] = GemmSeg{RH[l], WF[l], wp[l], wp[l + 1], wp[l]};
         a.seg[1] = GemmSeg{H[l], Vpart, wp[l], wp[l + 1], wp[l]};
+        seg3(a.seg[0], WF3[l], plane3_f(l), 0, wp[l]);
+        seg3(a.seg[1], WF3[l], plane3_f(l), 1, wp[l]);
       }
       a.skip = skip;
       a.ea.bias = v + offb[l];
@@ -608,6 +674,8 @@ struct trpo_engine {
       a.nseg = 2;
       a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
       a.seg[1] = GemmSeg{D[l], WB[l] + (size_t)wp[l + 1] * wp[l], wp[l + 1], wp[l], wp[l + 1]};
+      seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
+      seg3(a.seg[1], WB3[l], plane3_b(l), 1, wp[l + 1]);
       a.skip = skip;
       a.epi = RowEpi::kRBwd;
       a.ea.H = H[l];
@@ -658,7 +726,8 @@ struct trpo_engine {
     require_batch();
     PackArgs pa = pack_args(WFt, nullptr);
     launch_pack(pa, th, 0, nullptr, stream);
-    forward(WFt, th, RH, RowEpi::kLossHead, "ls_fwd");
+    split_parts(true, false, false, false, WFt, WFt3, nullptr, "split_t");
+    forward(WFt, WFt3, th, RH, RowEpi::kLossHead, "ls_fwd");
     reduce_losses(1, nullptr);
   }
 
@@ -1167,16 +1236,28 @@ int trpo_discount(const double* x, const uint8_t* starts, int64_t n, double gamm
   });
 }
 
+static int* option_slot(const std::string& k) {
+  if (k == "row_cfg") return &g_options.row_cfg;
+  if (k == "wg_cfg") return &g_options.wg_cfg;
+  if (k == "fused_head") return &g_options.fused_head;
+  if (k == "head_bwd") return &g_options.head_bwd;
+  if (k == "narrow_pf") return &g_options.narrow_pf;
+  if (k == "split_mfma") return &g_options.split_mfma;
+  if (k == "split_wg") return &g_options.split_wg;
+  throw ArgError("unknown option " + k);
+}
+
 int trpo_set_option(const char* name, int value) {
   return guarded([&] {
     REQUIRE(name, "NULL argument");
-    const std::string k(name);
-    if (k == "row_cfg") g_options.row_cfg = value;
-    else if (k == "wg_cfg") g_options.wg_cfg = value;
-    else if (k == "fused_head") g_options.fused_head = value;
-    else if (k == "head_bwd") g_options.head_bwd = value;
-    else if (k == "narrow_pf") g_options.narrow_pf = value;
-    else throw ArgError("unknown option " + k);
+    *option_slot(name) = value;
+  });
+}
+
+int trpo_get_option(const char* name, int* value) {
+  return guarded([&] {
+    REQUIRE(name && value, "NULL argument");
+    *value = *option_slot(name);
   });
 }
 

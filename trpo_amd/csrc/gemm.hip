@@ -32,7 +32,8 @@ static int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
-                     env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1)};
+                     env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
+                     env_int("TRPO_SPLIT_WG", 2)};
 
 namespace {
 
@@ -201,6 +202,119 @@ __device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
   nt = swz - mt * ntn;
 }
 
+// Fused epilogue of a row-GEMM tile.  The accumulator layout (col = lane&31,
+// row = (r&3) + 8(r>>2) + 4(lane>>5)) is the same for the f32 (32x32x2) and the
+// bf16 (32x32x16) MFMA, so both row-GEMM kernels share it.
+template <int WM, int WN, int TM, int TN, int EPI>
+__device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&acc)[TM][TN], int m0, int n0,
+                                             int wm, int wn, int lr, int lh) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  const int M = args.M;
+  const RowEpiArgs& e = args.ea;
+  if constexpr (EPI >= (int)RowEpi::kPrepHead) {
+    static_assert(WN == 1 && TN == 1, "row-wise head epilogue needs the whole row in one wave half");
+    const int col = n0 + lr;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r]);
+      }
+  } else {
+    const bool fulln = (n0 + BN <= args.Npad);
+    if (fulln) {
+      // Full-width tile: every epilogue operand goes through a per-block buffer
+      // descriptor (base = row m0, num_records = the rows this tile owns), so a
+      // load/store is one buffer op with a lane-constant voffset and a per-row SGPR
+      // soffset; rows past M fall outside the descriptor (loads read 0, stores are
+      // dropped) -- no per-element predicate, no 64-bit address math, and all 16
+      // loads of a chunk stay in flight.
+      const int ldo = e.ldo;
+      const int Mt = M - m0 < BM ? M - m0 : BM;
+      const int tile_bytes = Mt * ldo * 4;
+      auto mk = [&](const float* ptr) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
+      };
+      constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
+                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd;
+      constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
+      constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd;
+      // descriptors of operands an epilogue does not use alias out0 and are never touched
+      const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
+      const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
+      const __amdgpu_buffer_rsrc_t rE = mk(kRB ? e.E : e.out0);
+      const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
+      const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
+      const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
+      auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+      };
+      auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+      };
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
+        float bv = 0.0f;
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden)
+          bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
+        const int vo = vbase + tn * 128;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          float o0[16], o1[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+            const float v = acc[tm][tn][r];
+            if constexpr (EPI == (int)RowEpi::kTanh) {
+              o0[r] = tanhf(v + bv);
+            } else if constexpr (EPI == (int)RowEpi::kRHidden) {
+              o0[r] = one_minus_sq(ld(rH, vo, so)) * (v + bv);
+            } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
+              const float h = ld(rH, vo, so);
+              o0[r] = v * one_minus_sq(h);
+              o1[r] = -2.0f * v * h;
+            } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
+              o0[r] = v * one_minus_sq(ld(rH, vo, so));
+            } else {
+              o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+            st(o0[r], rO0, vo, so);
+            if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
+          }
+        }
+      }
+    } else {
+      // partial-width tile (odd layer widths): predicated path
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
+        const bool real = col < args.N;
+        const bool colv = col < args.Npad;
+        const int colc = colv ? col : 0;
+        float bv = 0.0f;
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden) bv = e.bias[real ? col : 0];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < M && colv) {
+              float o0, o1;
+              epi_elem_v<EPI>(e, (size_t)row * e.ldo + colc, real, acc[tm][tn][r], real ? bv : 0.0f, o0, o1);
+              epi_store<EPI>(e, (size_t)row * e.ldo + col, o0, o1);
+            }
+          }
+      }
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int BK, int EPI, int PF = 1>
 __global__ void __launch_bounds__(WM* WN * 64, (TM * TN >= 8 || EPI == 2) ? 2 : 4)   // waves / SIMD
 rowgemm_kernel(const RowGemmArgs args) {
@@ -317,140 +431,478 @@ rowgemm_kernel(const RowGemmArgs args) {
       Stage S;
       gload(S, 0);
       sstore(S, 0);
-      __syncthreads();
+      lds_barrier();
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
         compute(t & 1);
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
-        __syncthreads();
+        lds_barrier();
       }
     } else {
       // two stages in flight: tile t in LDS buffer t&1, tile t+1 in a register stage,
       // tile t+2 being loaded; unrolled by two so each stage has a static name
       Stage S0, S1;
       gload(S0, 0);
-      if (1 < ntiles) gload(S1, 1);
+      gload(S1, ntiles > 1 ? 1 : 0);
       sstore(S0, 0);
-      __syncthreads();
+      lds_barrier();
       int t = 0;
       for (; t + 1 < ntiles; t += 2) {
-        if (t + 2 < ntiles) gload(S0, t + 2);
+        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
         compute(0);
         sstore(S1, 1);
-        __syncthreads();
-        if (t + 3 < ntiles) gload(S1, t + 3);
+        lds_barrier();
+        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
         compute(1);
         if (t + 2 < ntiles) sstore(S0, 0);
-        __syncthreads();
+        lds_barrier();
       }
       if (t < ntiles) compute(0);
     }
   }
 
   // ---- epilogue -----------------------------------------------------------
-  const RowEpiArgs& e = args.ea;
-  if constexpr (EPI >= (int)RowEpi::kPrepHead) {
-    static_assert(WN == 1 && TN == 1, "row-wise head epilogue needs the whole row in one wave half");
-    const int col = n0 + lr;
+  row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+}
+
+
+// ---------------------------------------------------------------------------
+// Split-bf16 row GEMM.  CDNA4 has no reduced-precision f32 MFMA, but bf16 MFMA
+// runs at 16x the f32 rate.  Each f32 operand x is split exactly into three
+// bf16 pieces x = h + m + l + O(2^-27 |x|) (h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m); both differences are exact in f32) and
+//     a*b ~= ah bh + (ah bm + am bh) + (ah bl + al bh + am bm)
+// keeps every product term down to 2^-18 relative; the dropped ones (am bl,
+// al bm, al bl) are < 2^-26 relative, below the f32 rounding of the sum.  The
+// pieces' products are exact in the MFMA's f32 accumulation, so the result
+// matches an f32 GEMM to f32 rounding at 16/6 = 2.7x its MFMA peak.
+//
+// A (activations, f32 in HBM) is split while staging global -> LDS; B (packed
+// weights) is pre-split by split_b_kernel into [3][Npad][ldk] planes.
+// v_mfma_f32_32x32x16_bf16: lane l (r = l&31, h = l>>5) holds A[r][8h..8h+7]
+// and B[8h..8h+7][col r] - one ds_read_b128 per plane from [row][k] images.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) {
+  return __builtin_bit_cast(float, (unsigned)b << 16);
+}
+__device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+  h = bf16_bits(x);
+  const float r1 = x - bf16_val(h);
+  m = bf16_bits(r1);
+  const float r2 = r1 - bf16_val(m);
+  l = bf16_bits(r2);
+}
+
+// LDS images are [row][16 k] bf16 (32-B rows, no padding); the two 16-B k-chunks of
+// a row swap places on odd 8-row groups, so the 16 lanes of a ds_read_b128 phase
+// (rows r..r+15, one chunk) hit 16 distinct bank groups.
+__device__ __forceinline__ int swz16(int row, int chunk) { return row * 16 + ((chunk ^ ((row >> 3) & 1)) << 3); }
+
+template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF>
+__global__ void __launch_bounds__(WM* WN * 64, OCC)   // OCC waves / SIMD
+rowgemm3_kernel(const RowGemmArgs args) {
+  constexpr int BK = 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
+  constexpr int APL = BM * BK, BPL = BN * BK;     // one plane
+  constexpr int STG = 3 * (APL + BPL);
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STG];
+  if (args.skip && *args.skip) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  int mt, ntile;
+  tile_of((args.Npad + BN - 1) / BN, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int M = args.M;
+
+  const int nt0 = (args.seg[0].K + BK - 1) / BK;
+  const int nt1 = args.nseg > 1 ? (args.seg[1].K + BK - 1) / BK : 0;
+  const int ntiles = nt0 + nt1;
+
+  f32x16 acc[TM][TN];
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r]);
-      }
-  } else {
-    const bool fulln = (n0 + BN <= args.Npad);
-    if (fulln) {
-      // Full-width tile: every epilogue operand goes through a per-block buffer
-      // descriptor (base = row m0, num_records = the rows this tile owns), so a
-      // load/store is one buffer op with a lane-constant voffset and a per-row SGPR
-      // soffset; rows past M fall outside the descriptor (loads read 0, stores are
-      // dropped) -- no per-element predicate, no 64-bit address math, and all 16
-      // loads of a chunk stay in flight.
-      const int ldo = e.ldo;
-      const int Mt = M - m0 < BM ? M - m0 : BM;
-      const int tile_bytes = Mt * ldo * 4;
-      auto mk = [&](const float* ptr) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
-      };
-      constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
-                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd;
-      constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
-      constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd;
-      // descriptors of operands an epilogue does not use alias out0 and are never touched
-      const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
-      const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
-      const __amdgpu_buffer_rsrc_t rE = mk(kRB ? e.E : e.out0);
-      const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
-      const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
-      const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
-      auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
-      };
-      auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
-      };
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  constexpr int AF4 = BM * BK / 4;          // f32x4 of A per k-tile
+  constexpr int BC = 3 * BN * (BK / 8);     // 16-B chunks of B planes per k-tile
+  constexpr int AP = (AF4 + NT - 1) / NT, BP = (BC + NT - 1) / NT;
+  struct Stage {
+    f32x4 ra[AP];
+    u16x8 rb[BP];
+    bool oka[AP], okb[BP];
+  };
+  auto gload = [&](Stage& st, int t) {
+    const bool s1 = t >= nt0;
+    const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
+    const float* Ap = sg.A;
+    const int lda = sg.lda, K = sg.K;
+    const uint16_t* B3 = sg.B3;
+    const int ldk = sg.ldk, plane = sg.plane;
+    const int k0 = (s1 ? t - nt0 : t) * BK;
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
-        float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden)
-          bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
-        const int vo = vbase + tn * 128;
+    for (int i = 0; i < AP; ++i) {
+      const int f = tid + i * NT;
+      const int r = f / (BK / 4), kq = f % (BK / 4);
+      const int row = m0 + r, k = k0 + 4 * kq;
+      const bool ok = (AF4 % NT == 0 || f < AF4) && row < M && k < K;
+      st.ra[i] = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
+      st.oka[i] = ok;
+    }
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          float o0[16], o1[16];
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      const int p = f / (BN * 2), rem = f % (BN * 2);
+      const int n = rem >> 1, kh = rem & 1;
+      const bool ok = (BC % NT == 0 || f < BC) && n0 + n < args.Npad;
+      st.rb[i] = *reinterpret_cast<const u16x8*>(B3 + (ok ? (size_t)p * plane + (size_t)(n0 + n) * ldk + k0 + 8 * kh : 0));
+      st.okb[i] = ok;
+    }
+  };
+  auto sstore = [&](const Stage& st, int buf) {
+    unsigned short* As = smem + buf * STG;
+    unsigned short* Bs = As + 3 * APL;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
-            const float v = acc[tm][tn][r];
-            if constexpr (EPI == (int)RowEpi::kTanh) {
-              o0[r] = tanhf(v + bv);
-            } else if constexpr (EPI == (int)RowEpi::kRHidden) {
-              o0[r] = one_minus_sq(ld(rH, vo, so)) * (v + bv);
-            } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
-              const float h = ld(rH, vo, so);
-              o0[r] = v * one_minus_sq(h);
-              o1[r] = -2.0f * v * h;
-            } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
-              o0[r] = v * one_minus_sq(ld(rH, vo, so));
-            } else {
-              o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
-            }
-          }
+    for (int i = 0; i < AP; ++i) {
+      const int f = tid + i * NT;
+      if (AF4 % NT == 0 || f < AF4) {
+        const int r = f / (BK / 4), kq = f % (BK / 4);
+        const f32x4 x = st.oka[i] ? st.ra[i] : f32x4{};
+        u16x4 h, m, l;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
-            st(o0[r], rO0, vo, so);
-            if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
-          }
+        for (int j = 0; j < 4; ++j) {
+          unsigned short hh, mm, ll;
+          split3(x[j], hh, mm, ll);
+          h[j] = hh;
+          m[j] = mm;
+          l[j] = ll;
         }
-      }
-    } else {
-      // partial-width tile (odd layer widths): predicated path
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
-        const bool real = col < args.N;
-        const bool colv = col < args.Npad;
-        const int colc = colv ? col : 0;
-        float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden) bv = e.bias[real ? col : 0];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (row < M && colv) {
-              float o0, o1;
-              epi_elem_v<EPI>(e, (size_t)row * e.ldo + colc, real, acc[tm][tn][r], real ? bv : 0.0f, o0, o1);
-              epi_store<EPI>(e, (size_t)row * e.ldo + col, o0, o1);
-            }
-          }
+        unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
+        *reinterpret_cast<u16x4*>(dst) = h;
+        *reinterpret_cast<u16x4*>(dst + APL) = m;
+        *reinterpret_cast<u16x4*>(dst + 2 * APL) = l;
       }
     }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      if (BC % NT == 0 || f < BC) {
+        const int p = f / (BN * 2), rem = f % (BN * 2);
+        const int n = rem >> 1, kh = rem & 1;
+        *reinterpret_cast<u16x8*>(Bs + p * BPL + swz16(n, kh)) = st.okb[i] ? st.rb[i] : u16x8{};
+      }
+    }
+  };
+  auto compute = [&](int buf) {
+    const unsigned short* As = smem + buf * STG;
+    const unsigned short* Bs = As + 3 * APL;
+    // fragments streamed per output column tile to keep few registers live
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      bf16x8 b[3];
+      const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        bf16x8 a[3];
+        const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
+        // smallest terms first
+        f32x16 c = acc[tm][tn];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+        acc[tm][tn] = c;
+      }
+    }
+  };
+
+  if (ntiles > 0) {
+    if constexpr (PF == 1) {
+      Stage S;
+      gload(S, 0);
+      sstore(S, 0);
+      lds_barrier();
+      for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(S, t + 1);
+        compute(t & 1);
+        if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
+        lds_barrier();
+      }
+    } else {
+      // two k-tiles of loads in flight (see rowgemm_kernel)
+      Stage S0, S1;
+      gload(S0, 0);
+      gload(S1, ntiles > 1 ? 1 : 0);
+      sstore(S0, 0);
+      lds_barrier();
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
+        compute(0);
+        sstore(S1, 1);
+        lds_barrier();
+        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+        compute(1);
+        if (t + 2 < ntiles) sstore(S0, 0);
+        lds_barrier();
+      }
+      if (t < ntiles) compute(0);
+    }
   }
+  row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+}
+
+
+// ---------------------------------------------------------------------------
+// Split-bf16 weight gradient: C[i][j] = sum_rows A[r][i] B[r][j] with the rows as
+// the MFMA k dimension (see rowgemm3_kernel for the split arithmetic).  Both
+// operands are row-major activations, so staging transposes: a thread owns one
+// column and 8 consecutive rows (8 coalesced dword loads), splits them and
+// writes one 16-B k-chunk per plane of the [column][16 rows] LDS image.
+// ---------------------------------------------------------------------------
+template <int WM, int WN, int TM, int TN, int OCC, int PF>
+__global__ void __launch_bounds__(WM* WN * 64, OCC)
+wgrad3_kernel(const WGradArgs args) {
+  constexpr int BK = 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
+  constexpr int APL = BM * BK, BPL = BN * BK;
+  constexpr int STG = 3 * (APL + BPL);
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STG];
+  __shared__ float cs_sh[2][BN];
+  if (args.skip && *args.skip) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+  const int r0 = split * args.rows_per_split;
+  const int r1 = min(args.rows, r0 + args.rows_per_split);
+  const int nk = r1 > r0 ? (r1 - r0 + BK - 1) / BK : 0;
+  const int ntiles = nk * args.nseg;
+  const bool do_colsum = (blockIdx.x == 0);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  constexpr int AI = 2 * BM, BI = 2 * BN;   // (column, 8-row group) items per k-tile
+  constexpr int AP = (AI + NT - 1) / NT, BP = (BI + NT - 1) / NT;
+  float csum[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) csum[i] = 0.0f;
+  struct Stage {
+    float va[AP][8], vb[BP][8];
+    int nv;          // valid rows of the tile (>= 16: all)
+    bool cs;         // this tile belongs to the column-summed segment
+  };
+  auto gload = [&](Stage& st, int t) {
+    const int sg = t / nk;
+    const int kt = t - sg * nk;
+    const float* Ap = sg ? args.seg[1].A : args.seg[0].A;
+    const float* Bp = sg ? args.seg[1].B : args.seg[0].B;
+    const int lda = sg ? args.seg[1].lda : args.seg[0].lda;
+    const int ldb = sg ? args.seg[1].ldb : args.seg[0].ldb;
+    const int rb0 = r0 + kt * BK;
+    st.nv = r1 - rb0;
+    st.cs = do_colsum && sg == args.colsum_seg;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int f = tid + i * NT;
+      const int c = f % BM, g = f / BM;
+      const bool okc = (AI % NT == 0 || f < AI) && m0 + c < args.Mpad;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = rb0 + 8 * g + q;
+        const bool ok = okc && r < r1;
+        st.va[i][q] = Ap[(size_t)(ok ? r : r0) * lda + (ok ? m0 + c : 0)];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      const int c = f % BN, g = f / BN;
+      const bool okc = (BI % NT == 0 || f < BI) && n0 + c < args.Npad;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = rb0 + 8 * g + q;
+        const bool ok = okc && r < r1;
+        st.vb[i][q] = Bp[(size_t)(ok ? r : r0) * ldb + (ok ? n0 + c : 0)];
+      }
+    }
+  };
+  auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int nv) {
+    u16x8 h, m, l;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float x = (8 * g + q < nv) ? v[q] : 0.0f;
+      unsigned short hh, mm, ll;
+      split3(x, hh, mm, ll);
+      h[q] = hh;
+      m[q] = mm;
+      l[q] = ll;
+    }
+    unsigned short* dst = base + swz16(c, g);
+    *reinterpret_cast<u16x8*>(dst) = h;
+    *reinterpret_cast<u16x8*>(dst + plane_elems) = m;
+    *reinterpret_cast<u16x8*>(dst + 2 * plane_elems) = l;
+  };
+  auto sstore = [&](const Stage& st, int buf) {
+    unsigned short* As = smem + buf * STG;
+    unsigned short* Bs = As + 3 * APL;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int f = tid + i * NT;
+      if (AI % NT == 0 || f < AI) {
+        const int c = f % BM, g = f / BM;
+        // an invalid column holds finite clamped data; zero it through nv = 0
+        put(As, APL, c, g, st.va[i], m0 + c < args.Mpad ? st.nv : 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      if (BI % NT == 0 || f < BI) {
+        const int c = f % BN, g = f / BN;
+        const int nv = n0 + c < args.Npad ? st.nv : 0;
+        put(Bs, BPL, c, g, st.vb[i], nv);
+        if (st.cs) {
+          float cs = 0.0f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) cs += (8 * g + q < nv) ? st.vb[i][q] : 0.0f;
+          csum[i] += cs;
+        }
+      }
+    }
+  };
+  auto compute = [&](int buf) {
+    const unsigned short* As = smem + buf * STG;
+    const unsigned short* Bs = As + 3 * APL;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      bf16x8 b[3];
+      const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        bf16x8 a[3];
+        const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
+        f32x16 c = acc[tm][tn];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+        acc[tm][tn] = c;
+      }
+    }
+  };
+
+  if (ntiles > 0) {
+    if constexpr (PF == 1) {
+      Stage S;
+      gload(S, 0);
+      sstore(S, 0);
+      lds_barrier();
+      for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(S, t + 1);
+        compute(t & 1);
+        if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
+        lds_barrier();
+      }
+    } else {
+      Stage S0, S1;
+      gload(S0, 0);
+      gload(S1, ntiles > 1 ? 1 : 0);
+      sstore(S0, 0);
+      lds_barrier();
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);
+        compute(0);
+        sstore(S1, 1);
+        lds_barrier();
+        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+        compute(1);
+        if (t + 2 < ntiles) sstore(S0, 0);
+        lds_barrier();
+      }
+      if (t < ntiles) compute(0);
+    }
+  }
+
+  float* out = args.slab + (size_t)split * args.slab_stride;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int j = n0 + wn * TN * 32 + tn * 32 + lr;
+      if (j >= args.Nb) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (i < args.Ma) out[args.off_w + (int64_t)i * args.Nb + j] = acc[tm][tn][r];
+      }
+    }
+  if (do_colsum) {
+    // column sums: the two 8-row groups of a column, combined in a fixed order
+#pragma unroll
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      if (BI % NT == 0 || f < BI) cs_sh[f / BN][f % BN] = csum[i];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT)
+      if (n0 + c < args.Nb) out[args.off_b + n0 + c] = cs_sh[0][c] + cs_sh[1][c];
+  }
+}
+
+// One block per (64-column group of one job's planes, job); each thread writes one
+// 16-B chunk (8 consecutive k) of the three planes of one column.
+__global__ void __launch_bounds__(256) split_b_kernel(const SplitArgs a, const int* skip) {
+  if (skip && *skip) return;
+  const SplitJob& j = a.job[blockIdx.y];
+  const int nchunk = j.ldk / 8;
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  // lanes run over columns first so the f32 reads of one k row coalesce
+  const int n = f % j.Npad, c = f / j.Npad;
+  if (c >= nchunk) return;
+  u16x8 h, m, l;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = 8 * c + q;
+    const float x = k < j.K ? j.B[(size_t)k * j.ldb + n] : 0.0f;
+    unsigned short hh, mm, ll;
+    split3(x, hh, mm, ll);
+    h[q] = hh;
+    m[q] = mm;
+    l[q] = ll;
+  }
+  const size_t plane = (size_t)j.Npad * j.ldk;
+  uint16_t* dst = j.B3 + (size_t)n * j.ldk + 8 * c;
+  *reinterpret_cast<u16x8*>(dst) = h;
+  *reinterpret_cast<u16x8*>(dst + plane) = m;
+  *reinterpret_cast<u16x8*>(dst + 2 * plane) = l;
 }
 
 // ---------------------------------------------------------------------------
@@ -574,29 +1026,29 @@ wgrad_kernel(const WGradArgs args) {
       Stage S;
       gload(S, 0);
       sstore(S, 0);
-      __syncthreads();
+      lds_barrier();
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
         compute(t & 1, cs_of(t));
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
-        __syncthreads();
+        lds_barrier();
       }
     } else {
       Stage S0, S1;
       gload(S0, 0);
-      if (1 < ntiles) gload(S1, 1);
+      gload(S1, ntiles > 1 ? 1 : 0);
       sstore(S0, 0);
-      __syncthreads();
+      lds_barrier();
       int t = 0;
       for (; t + 1 < ntiles; t += 2) {
-        if (t + 2 < ntiles) gload(S0, t + 2);
+        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
         compute(0, cs_of(t));
         sstore(S1, 1);
-        __syncthreads();
-        if (t + 3 < ntiles) gload(S1, t + 3);
+        lds_barrier();
+        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
         compute(1, cs_of(t + 1));
         if (t + 2 < ntiles) sstore(S0, 0);
-        __syncthreads();
+        lds_barrier();
       }
       if (t < ntiles) compute(0, cs_of(t));
     }
@@ -628,12 +1080,32 @@ void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
 
 int wide_cfg() { return g_options.row_cfg; }
 
+template <int WM, int WN, int TM, int TN, int EPI, int OCC = 2, int PF = 1>
+void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  for (int i = 0; i < a.nseg; ++i)
+    if (!a.seg[i].B3 || a.seg[i].ldk < ((a.seg[i].K + 15) / 16) * 16 || a.seg[i].ldk % 8)
+      throw std::runtime_error("split-bf16 row GEMM: segment without B planes");
+  const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
+  hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, s, a);
+}
+
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   if constexpr (EPI >= (int)RowEpi::kPrepHead) {
     if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
     if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
+  } else if (rowgemm_uses_split(a.Npad, a.epi)) {
+    switch (g_options.split_mfma) {
+      case 2: launch_row3_cfg<4, 2, 2, 4, EPI>(a, s); break;   // 256 x 256
+      case 3: launch_row3_cfg<2, 2, 2, 2, EPI>(a, s); break;   // 128 x 128
+      case 4: launch_row3_cfg<4, 2, 2, 2, EPI>(a, s); break;   // 256 x 128
+      case 5: launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s); break;   // 256 x 256, 2 k-tiles in flight
+      case 6: launch_row3_cfg<2, 4, 2, 2, EPI, 2, 2>(a, s); break;   // 128 x 256, 2 k-tiles in flight
+      case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
+      default: launch_row3_cfg<2, 4, 2, 2, EPI>(a, s); break;  // 128 x 256
+    }
   } else {
     if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
     else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
@@ -660,7 +1132,31 @@ void launch_wg_cfg(const WGradArgs& a, hipStream_t s) {
 
 int wg_cfg() { return g_options.wg_cfg; }
 
+template <int WM, int WN, int TM, int TN, int OCC, int PF>
+void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  if (a.rows_per_split % 16) throw std::runtime_error("split-bf16 wgrad: rows_per_split % 16");
+  dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
+  hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF>), grid, dim3(WM * WN * 64), 0, s, a);
+}
+
 }  // namespace
+
+bool rowgemm_uses_split(int Npad, RowEpi epi) {
+  return g_options.split_mfma != 0 && Npad > 128 && (int)epi < (int)RowEpi::kPrepHead;
+}
+
+void launch_split_b(const SplitArgs& a, const int* skip, hipStream_t s) {
+  if (a.n <= 0) return;
+  int maxb = 1;
+  for (int i = 0; i < a.n; ++i) {
+    const SplitJob& j = a.job[i];
+    if (j.ldk % 8 || j.ldk < ((j.K + 15) / 16) * 16) throw std::runtime_error("split_b: bad ldk");
+    const int b = (j.Npad * (j.ldk / 8) + 255) / 256;
+    maxb = b > maxb ? b : maxb;
+  }
+  hipLaunchKernelGGL(split_b_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, skip);
+}
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
@@ -691,6 +1187,18 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
   } else if (Np <= 128) {
     if (Mp <= 64) launch_wg_cfg<1, 2, 2, 2>(a, s);          // 64 x 128
     else launch_wg_cfg<2, 2, 2, 2>(a, s);                   // 128 x 128
+  } else if (g_options.split_wg != 0) {
+    // split-bf16 tiles
+    if (Mp <= 128) {
+      if (g_options.split_wg == 2) launch_wg3_cfg<2, 4, 2, 2, 2, 2>(a, s);   // 128 x 256, 2 stages
+      else launch_wg3_cfg<2, 4, 2, 2, 2, 1>(a, s);                           // 128 x 256
+    } else {
+      switch (g_options.split_wg) {
+        case 2: launch_wg3_cfg<4, 2, 2, 4, 2, 2>(a, s); break;   // 256 x 256, 2 stages
+        case 3: launch_wg3_cfg<2, 4, 2, 2, 2, 1>(a, s); break;   // 128 x 256
+        default: launch_wg3_cfg<4, 2, 2, 4, 2, 1>(a, s); break;  // 256 x 256
+      }
+    }
   } else {
     if (Mp <= 128) {
       if (g_options.narrow_pf == 2) launch_wg_cfg<2, 4, 2, 2, 16, 2>(a, s);   // 128 x 256, 2 stages

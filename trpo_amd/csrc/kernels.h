@@ -18,6 +18,8 @@ struct Options {
   int fused_head;  // engine: last-layer R-fwd + R-bwd + wgrad in one LDS-resident kernel
   int head_bwd;    // engine: last-layer R-bwd + wgrad in one kernel
   int narrow_pf;   // prefetch depth (1 or 2) of the memory-bound narrow tiles (softmax head, 128x256 wgrad)
+  int split_mfma;  // row GEMMs with N > 128 on bf16 MFMA with fp32 operands split 3 ways (hi+mid+lo)
+  int split_wg;    // weight gradients with fan_out > 128 on the split-bf16 MFMA (tile choice 1..3)
 };
 extern Options g_options;
 
@@ -28,6 +30,10 @@ struct GemmSeg {
   const float* A;  // [M][lda]
   const float* B;  // [K][ldb]
   int lda, ldb, K; // K multiple of 4
+  // split-bf16 GEMM only: B as three bf16 planes (hi, mid, lo) [3][Npad][ldk], k contiguous,
+  // zero for k >= K (see launch_split_b); plane = elements per plane
+  const uint16_t* B3 = nullptr;
+  int ldk = 0, plane = 0;
 };
 
 enum class RowEpi : int {
@@ -69,6 +75,22 @@ struct RowGemmArgs {
 };
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
+// true when launch_rowgemm will take the split-bf16 path for this shape (the segments' B3 must be set)
+bool rowgemm_uses_split(int Npad, RowEpi epi);
+
+// Split fp32 matrices B [K][ldb] (columns [0, Npad)) into bf16 planes B3 [3][Npad][ldk]
+// (hi = bf16(b), mid = bf16(b - hi), lo = bf16(b - hi - mid); k >= K zero-filled).
+struct SplitJob {
+  const float* B;
+  uint16_t* B3;
+  int K, Npad, ldb, ldk;
+};
+constexpr int kMaxSplitJobs = 16;
+struct SplitArgs {
+  int n;
+  SplitJob job[kMaxSplitJobs];
+};
+void launch_split_b(const SplitArgs& a, const int* skip, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Weight-gradient GEMM (split-K over rows):
