@@ -19,7 +19,14 @@ states are split row-wise (path-aligned), so ``scaling`` is "strong".
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel (largest
 share of HIP-event time over the timed region, on the engine's stream):
-algorithmic FLOPs per launch / average launch time vs the f32 MFMA peak.
+algorithmic FLOPs per launch / average launch time vs the ceiling of the MFMA
+path that kernel runs on -- the f32 MFMA peak (157.3 TF/s), or for the
+split-bf16 GEMMs (fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMA
+products per fp32 product) the bf16 dense peak / 6 = 416.7 TF/s of fp32 work.
+``traffic`` is the HBM bytes per launch of that kernel measured by rocprofv3
+FETCH_SIZE / WRITE_SIZE passes of this same command (tools/prof.sh ->
+tools/pmc_traffic.py -> profiles/<round>/traffic.json), when a committed file
+matches the workload.
 ``cpu_baseline`` (N=1, rank 0 only) times the TF-faithful float32 CPU mirror of
 the reference (oracle/tf_graph_torch.py: every FVP recomputes forward + both
 backward passes, as each session.run does) on a bounded row sample and
@@ -40,6 +47,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "TRPO updates/sec (10-iter CG + linesearch) at N states; FVP GB/s vs HBM peak"
 PEAK_F32_TFLOPS = 157.3        # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
+PEAK_BF16_TFLOPS = 2500.0      # MI355X_MICROARCH.md: BF16 MFMA dense peak
+SPLIT_PRODUCTS = 6             # hh, hm, mh, hl, lh, mm per fp32 product
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / SPLIT_PRODUCTS
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_LEN = 200              # CartPole-v0 cap
 
@@ -74,6 +84,43 @@ def tag_flops(tag: str, widths, n: int) -> float:
     if role == "fvp_headbwd":       # R-backward (2ab) + wgrad (2ab) of the last layer
         return 2 * ab
     return 0.0
+
+
+def tag_is_split(tag: str, widths) -> bool:
+    """Whether the kernel behind a tag runs on the split-bf16 MFMA path (gemm.hip dispatch rules)."""
+    from trpo_amd._lib import get_option
+    role, _, l = tag.rpartition("_l")
+    if not l.isdigit():
+        return False
+    l = int(l)
+    pad = lambda v: (v + 3) // 4 * 4
+    a, b = pad(widths[l]), pad(widths[l + 1])
+    if role.endswith("wgrad"):
+        return get_option("split_wg") != 0 and b > 128
+    if role in ("fvp_head", "fvp_headbwd"):
+        return False
+    last = l == len(widths) - 2
+    out = a if role in ("bwd", "pg_bwd", "fvp_rbwd") else b
+    head = last and role in ("fwd", "ls_fwd", "fvp_rfwd")
+    return get_option("split_mfma") != 0 and out > 128 and not head
+
+
+def tag_peak(tag: str, widths) -> float:
+    return PEAK_SPLIT_TFLOPS if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
+
+
+def committed_traffic(config: str, rows: int, tag: str):
+    """Per-launch HBM bytes of `tag` from the newest matching profiles/*/traffic.json."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") == config and d.get("rows") == rows and tag in d.get("tags", {}):
+            best = (os.path.relpath(f, ROOT), d["tags"][tag])
+    return best
 
 
 def fvp_flops_per_row(widths) -> float:
@@ -226,7 +273,12 @@ def main():
         avg_s = tot_ms / cnt / 1e3
         fl = tag_flops(dom, widths, n)
         achieved = fl / avg_s / 1e12
+        peak = tag_peak(dom, widths)
         upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / args.steps
+        # seconds one update would take with every kernel at its path's peak
+        upd_peak_s = sum(tag_flops(t, widths, n) * c / (tag_peak(t, widths) * 1e12)
+                         for t, (c, _) in kernel_tags.items()) / args.steps
+        tr = committed_traffic(args.config, N, dom) if world == 1 else None
         upd_s = elapsed / args.steps
         fvp_ms = sum(ms for t, (c, ms) in prof.items() if t.startswith("fvp_") or t == "reduce")
         fvp_calls = prof.get("fvp_wgrad_l0", [0, 0])[0]
@@ -244,6 +296,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
+            "arithmetic": "fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on bf16 MFMA with "
+                          "each fp32 operand split exactly into hi+mid+lo bf16 pieces (6 products, error below "
+                          "f32 MFMA's); narrower GEMMs on f32 MFMA; softmax heads and CG scalars in f64",
             "data": "synthetic (X~N(0,1), a~U{0..A-1}, rewards~U(0,1), paths of 200 steps, "
                     "random-init policy, pi_old = p(theta_0))",
             "config": {"workload": cfg["name"] + "; full update = discount+standardise+pg+10 CG+shs FVP+"
@@ -251,12 +306,17 @@ def main():
                        "n_states": N, "obs_dim": cfg["obs"], "hidden": cfg["hidden"], "n_actions": cfg["A"],
                        "num_params": eng.num_params, "cg_iters": 10, "residual_tol": 0.0,
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_F32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak,
+                         "traffic": tr[1]["traffic_bytes"] if tr else None,
+                         "peak_basis": ("split-bf16 MFMA: bf16 dense peak / 6 products" if peak == PEAK_SPLIT_TFLOPS
+                                        else "f32 MFMA peak"),
+                         "hbm_gbs_at_traffic": tr[1]["traffic_bytes"] / avg_s / 1e9 if tr else None,
+                         "traffic_source": tr[0] if tr else None,
                          "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt},
             "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
                                 "achieved_tflops": upd_flops * world / upd_s / 1e12,
-                                "frac_of_peak": upd_flops / upd_s / 1e12 / PEAK_F32_TFLOPS},
+                                "frac_of_peak": upd_peak_s / upd_s},
             "fvp": {"ms_per_fvp": fvp_s * 1e3, "gbps_algorithmic": fvp_bytes / fvp_s / 1e9,
                     "hbm_frac": fvp_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
                     "tflops": fvp_flops_per_row(widths) * n / fvp_s / 1e12},

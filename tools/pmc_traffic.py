@@ -1,0 +1,89 @@
+"""Per-launch HBM traffic of the bench's hot kernels from rocprofv3 PMC passes (tools/prof.sh).
+
+    python tools/pmc_traffic.py gpurun_out/<name> profiles/<round>/traffic.json --config c4 --rows 8000000
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  MI355X_MICROARCH.md (HBM/rocprofv3):
+on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane) streaming reads, so
+read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for streaming stores.  The hot
+kernels' operand loads are 16 B/lane streams; their epilogue loads are 4 B/lane row
+segments (whole 128-B lines per 32 lanes), for which the same factor held: the
+R-backward launches read 2 x FETCH = 42.3 GB against 41.9 GB of algorithmic bytes.
+
+A bench tag is matched to dispatches by kernel name plus its position in the fixed
+launch order of one FVP (e.g. the two kRBwd row GEMMs of an FVP are l=2 then l=1).
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+# tag -> (kernel-name substring, period, phase): the phase-th of every `period` dispatches
+SPECS = {
+    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2>", 2, 1),
+    "fvp_rbwd_l2": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2>", 2, 0),
+    "fvp_rfwd_l0": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2>", 2, 0),
+    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2>", 2, 1),
+    "fvp_rfwd_l2": ("rowgemm_kernel<4, 1, 2, 1, 16, 7, 1>", 1, 0),
+}
+# tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
+LONGEST = {
+    "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 2>",
+    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 2>",
+    "fvp_wgrad_l2": "wgrad_kernel<4, 1, 2, 1, 16, 1>",
+}
+
+
+def load(path, counter):
+    rows = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]),
+                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    rows.sort()
+    return rows
+
+
+def pick(rows, sub, period=None, phase=None, longest=False):
+    sel = [r for r in rows if sub in r[1]]
+    if longest and sel:
+        dmax = max(r[3] for r in sel)
+        sel = [r for r in sel if r[3] > 0.75 * dmax]
+    elif period:
+        sel = [r for i, r in enumerate(sel) if i % period == phase]
+    return sel
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc_dir")
+    ap.add_argument("out")
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--rows", type=int, default=8_000_000)
+    a = ap.parse_args()
+    fetch = load(os.path.join(a.pmc_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = load(os.path.join(a.pmc_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    res = {"config": a.config, "rows": a.rows, "source": a.pmc_dir,
+           "method": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streams), write = WRITE_SIZE; "
+                     "KiB -> bytes x 1024; mean over the matched launches", "tags": {}}
+    todo = [(t, s, p, ph, False) for t, (s, p, ph) in SPECS.items()] + \
+           [(t, s, None, None, True) for t, s in LONGEST.items()]
+    for tag, sub, period, phase, longest in todo:
+        f = pick(fetch, sub, period, phase, longest)
+        w = pick(write, sub, period, phase, longest)
+        if not f or not w:
+            continue
+        rd = 2 * 1024 * statistics.mean(r[2] for r in f)
+        wr = 1024 * statistics.mean(r[2] for r in w)
+        res["tags"][tag] = {"kernel": sub, "launches": len(f), "read_bytes": rd, "write_bytes": wr,
+                            "traffic_bytes": rd + wr, "pmc_run_ms": statistics.mean(r[3] for r in f)}
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
+    for t, v in res["tags"].items():
+        print(f"{t:14s} {v['launches']:4d}  read {v['read_bytes'] / 1e9:7.2f} GB  write {v['write_bytes'] / 1e9:6.2f} GB"
+              f"  {v['pmc_run_ms']:7.2f} ms")
+
+
+if __name__ == "__main__":
+    main()
