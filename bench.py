@@ -65,8 +65,19 @@ CONFIGS = {
 }
 
 
+def chain_flops_per_row(widths) -> float:
+    """Fused FVP chain (R-forward + R-head + R-backward): 2 a1 b1 + 8 sum_{l>=2} a_l b_l per state."""
+    f = 0.0
+    for l in range(len(widths) - 1):
+        ab = widths[l] * widths[l + 1]
+        f += 2 * ab if l == 0 else 8 * ab
+    return f
+
+
 def tag_flops(tag: str, widths, n: int) -> float:
     """Algorithmic FLOPs of one launch of the kernel behind a profile tag."""
+    if tag == "fvp_chain":
+        return n * chain_flops_per_row(widths)
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0
@@ -89,6 +100,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
 def tag_is_split(tag: str, widths) -> bool:
     """Whether the kernel behind a tag runs on the split-bf16 MFMA path (gemm.hip dispatch rules)."""
     from trpo_amd._lib import get_option
+    if tag == "fvp_chain":
+        return True
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return False

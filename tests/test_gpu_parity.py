@@ -268,23 +268,25 @@ def test_bad_actions_fail_loudly(gpu_available):
 
 
 @pytest.mark.parametrize("opts", [
-    {"fused_head": 1},                 # LDS-resident last-layer fusion (opt-in)
-    {"head_bwd": 1},                   # last-layer R-backward + wgrad in one kernel (opt-in)
+    {"chain": 2}, {"chain": 3},               # fused FVP chain forms (default 1 = auto)
+    {"chain": 0},                               # per-layer row-GEMM FVP
+    {"chain": 0, "fused_head": 1},     # LDS-resident last-layer fusion (opt-in)
+    {"chain": 0, "head_bwd": 1},       # last-layer R-backward + wgrad in one kernel (opt-in)
     {"narrow_pf": 2},                  # two-stage prefetch for the narrow memory-bound tiles
     {"row_cfg": 1}, {"row_cfg": 2}, {"row_cfg": 3}, {"row_cfg": 4}, {"row_cfg": 5},
     {"wg_cfg": 1},
-    {"split_mfma": 0}, {"split_mfma": 1}, {"split_mfma": 2}, {"split_mfma": 3}, {"split_mfma": 4},
-    {"split_mfma": 5}, {"split_mfma": 6}, {"split_mfma": 7},
+    {"split_mfma": 0}, {"chain": 0, "split_mfma": 1}, {"chain": 0, "split_mfma": 2}, {"split_mfma": 3},
+    {"split_mfma": 4}, {"chain": 0, "split_mfma": 5}, {"chain": 0, "split_mfma": 6}, {"split_mfma": 7},
     {"split_wg": 0}, {"split_wg": 1}, {"split_wg": 2}, {"split_wg": 3},
     {"split_mfma": 5, "split_wg": 1},
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
-    C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles."""
+    C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles and the widest chain."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg")}
+                                           "split_wg", "chain")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -326,6 +328,36 @@ def test_kernel_variants_parity(gpu_available, opts):
     finally:
         for k, v in defaults.items():
             set_option(k, v)
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (37, [200, 72, 144], 5, 1337),     # odd widths, 3 hidden layers, 16 register tiles, partial workgroup
+    (128, [256, 256], 18, 3001),       # C4 dims, two head tiles
+    (11, [64], 32, 500),               # one hidden layer (the reference policy's depth), A = 32
+    (5, [16, 16], 17, 129),            # narrowest tiles
+])
+def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
+    """The fused FVP chain (default) against the oracle and against the per-layer row-GEMM FVP."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n)
+    v = np.random.RandomState(n + 1).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
+    saved = get_option("chain")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("chain", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            out[mode] = e.fvp(v, 0.0)
+            e.close()
+    finally:
+        set_option("chain", saved)
+    assert_vec_close(out[1], ref, REL, f"chain Hv {obs} {hidden} {A}")
+    assert_vec_close(out[1], out[0], REL, f"chain vs row-GEMM Hv {obs} {hidden} {A}")
 
 
 def test_two_ranks_share_gpu_host_allreduce(gpu_available):

@@ -138,6 +138,20 @@ struct trpo_engine {
   bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
   bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
+  // fused FVP chain (chain.hip): weight images in consumption order + chunk table
+  int chain_otm = 0;         // register tiles per hidden layer; 0 = shape not eligible
+  uint16_t* chain_img = nullptr;
+  int* chain_tab = nullptr;
+  int chain_nchunks = 0;
+  bool chain_w_valid = false;   // theta parts of the images match theta
+  ChainImgArgs chain_jobs{};
+  // auto (option 1) takes the chain up to 8 register tiles (hidden widths <= 128), where it
+  // beats the per-layer row GEMMs; at 16 tiles its per-128-state weight re-streaming
+  // (~2 MB of bf16 planes per workgroup tile) costs more than the fusion saves
+  bool use_chain() const {
+    return chain_otm > 0 && (g_options.chain >= 2 || (g_options.chain == 1 && chain_otm <= 8));
+  }
+
   // profiling
   bool prof = false;
   struct Ev {
@@ -292,7 +306,61 @@ struct trpo_engine {
     head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
+    setup_chain();
     HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  // Weight-image layout of the fused FVP chain, in the order the kernel consumes
+  // chunks: R-forward F_0 (V_0), F_l (W_l, V_l) for l = 1..L-1, then R-backward
+  // B_l (W_l^T, V_l^T) for l = L-1..1.  Each segment is ceil(K/32) chunks of
+  // [3 planes][16*ceil(O/16) rows][32] bf16.
+  void setup_chain() {
+    if (L < 2 || w[L] > 32) return;
+    int hmax = 0;
+    for (int l = 1; l < L; ++l) hmax = std::max(hmax, w[l]);
+    const int otm = chain_max_tiles(hmax);
+    if (!otm) return;
+    std::vector<int> tab;
+    int64_t off16 = 0;
+    int nj = 0;
+    auto seg = [&](int l, int trans, int which) {
+      const int K = trans ? w[l + 1] : w[l], O = trans ? w[l] : w[l + 1];
+      const int kc = (K + 31) / 32, otp = (O + 15) / 16 * 16, csz = otp * 12;   // 16-B units per chunk
+      ChainImgJob& j = chain_jobs.job[nj++];
+      j.src_off = offW[l];
+      j.dst_off = off16 * 8;
+      j.K = K;
+      j.O = O;
+      j.ldw = w[l + 1];
+      j.trans = trans;
+      j.kc = kc;
+      j.otp = otp;
+      j.which = which;
+      j.pad = 0;
+      for (int c = 0; c < kc; ++c) {
+        tab.push_back((int)(off16 + (int64_t)c * csz));
+        tab.push_back(csz);
+      }
+      off16 += (int64_t)kc * csz;
+    };
+    seg(0, 0, 1);
+    for (int l = 1; l < L; ++l) {
+      seg(l, 0, 0);
+      seg(l, 0, 1);
+    }
+    for (int l = L - 1; l >= 1; --l) {
+      seg(l, 1, 0);
+      seg(l, 1, 1);
+    }
+    REQUIRE(nj <= kMaxChainJobs && off16 < (int64_t(1) << 31), "fvp chain: layout too large");
+    chain_jobs.n = nj;
+    chain_img = dalloc<uint16_t>((size_t)off16 * 8);
+    chain_tab = dalloc<int>(tab.size());
+    chain_jobs.img = chain_img;
+    HIPCHECK(hipMemcpyAsync(chain_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));   // `tab` is a local vector
+    chain_nchunks = (int)(tab.size() / 2);
+    chain_otm = otm;
   }
 
   void release() {
@@ -476,6 +544,7 @@ struct trpo_engine {
     PackArgs pa = pack_args(WF, &WB);
     launch_pack(pa, theta, 0, nullptr, stream);
     w3_valid = false;
+    chain_w_valid = false;
     ensure_w3();
     forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
     // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H
@@ -566,6 +635,10 @@ struct trpo_engine {
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
   void fvp(const float* v, float* out, const int* skip) {
     prepare();
+    if (use_chain()) {
+      fvp_chain(v, out, skip);
+      return;
+    }
     {
       PackArgs pa = pack_args(WF, &WB);
       launch_pack(pa, v, 1, skip, stream);
@@ -698,6 +771,59 @@ struct trpo_engine {
       else
         wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1]}, WSeg{H[l], RD[l], wp[l], wp[l + 1]}, 1,
                     skip, tag);
+    }
+    reduce_grad(out, skip);
+  }
+
+  // the same Hv with the row-local part (R-forward, R-head, R-backward) in one fused launch
+  void fvp_chain(const float* v, float* out, const int* skip) {
+    if (!chain_w_valid) {
+      Scope sp(this, "fvp_img_w");
+      launch_chain_img(chain_jobs, theta, v, 0, nullptr, stream);
+      check_launch();
+      chain_w_valid = true;
+    }
+    {
+      Scope sp(this, "fvp_img_v");
+      launch_chain_img(chain_jobs, theta, v, 1, skip, stream);
+      check_launch();
+    }
+    ChainArgs ca{};
+    ca.n = (int)n;
+    ca.L = L;
+    for (int l = 0; l <= L; ++l) {
+      ca.w[l] = w[l];
+      ca.ld[l] = wp[l];
+    }
+    ca.X = X;
+    for (int l = 0; l < L; ++l) {
+      ca.H[l] = H[l];
+      ca.RH[l] = RH[l];
+      ca.D[l] = D[l];
+      ca.E[l] = E[l];
+      ca.RD[l] = RD[l];
+      ca.offb[l] = offb[l];
+    }
+    ca.P = Pm;
+    ca.v = v;
+    ca.img = chain_img;
+    ca.tab = chain_tab;
+    ca.nchunks = chain_nchunks;
+    ca.invN = 1.0 / (double)n_global;
+    ca.skip = skip;
+    {
+      Scope sp(this, "fvp_chain");
+      launch_fvp_chain(ca, chain_otm, stream);
+      check_launch();
+    }
+    // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
+    for (int l = 0; l < L; ++l) {
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
+      if (l == 0)
+        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1]}, WSeg{}, 0, skip, tag);
+      else
+        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1]}, WSeg{H[l], RD[l], wp[l], wp[l + 1]}, 1, skip, tag);
     }
     reduce_grad(out, skip);
   }
@@ -1244,6 +1370,7 @@ static int* option_slot(const std::string& k) {
   if (k == "narrow_pf") return &g_options.narrow_pf;
   if (k == "split_mfma") return &g_options.split_mfma;
   if (k == "split_wg") return &g_options.split_wg;
+  if (k == "chain") return &g_options.chain;
   throw ArgError("unknown option " + k);
 }
 

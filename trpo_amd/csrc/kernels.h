@@ -20,6 +20,7 @@ struct Options {
   int narrow_pf;   // prefetch depth (1 or 2) of the memory-bound narrow tiles (softmax head, 128x256 wgrad)
   int split_mfma;  // row GEMMs with N > 128 on bf16 MFMA with fp32 operands split 3 ways (hi+mid+lo)
   int split_wg;    // weight gradients with fan_out > 128 on the split-bf16 MFMA (tile choice 1..3)
+  int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
 };
 extern Options g_options;
 
@@ -286,4 +287,52 @@ struct HeadBwdArgs {
   const int* skip;
 };
 void launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
+}  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Fused row-local FVP chain (chain.hip): R-forward through every layer, the
+// R-softmax head and the R-backward down to layer 1 in one launch, 16 states
+// per wave with activations carried in MFMA accumulator layout; writes RH_l and
+// RD_l for the weight-gradient GEMMs.  Eligible when hidden widths <= 256 and
+// n_actions <= 32.
+// ---------------------------------------------------------------------------
+struct ChainArgs {
+  int n, L;                          // rows of this shard; layers
+  int w[kMaxLayers + 1];             // widths [obs, hidden..., A]
+  int ld[kMaxLayers + 1];            // row strides pad4(w)
+  const float* X;
+  const float* H[kMaxLayers];        // H[l], l = 1..L-1
+  float* RH[kMaxLayers];             // RH[l], l = 1..L-1 (written)
+  const float* P;                    // softmax at theta
+  const float* D[kMaxLayers];        // D[l], l = 0..L-1 (width w[l+1])
+  const float* E[kMaxLayers];        // E[l], l = 0..L-2 (width w[l+1])
+  float* RD[kMaxLayers];             // RD[l], l = 0..L-1 (written)
+  const float* v;                    // tangent (flat), for the tangent biases
+  int64_t offb[kMaxLayers];          // bias offsets in the flat vector
+  const void* img;                   // weight images (16-B units)
+  const int* tab;                    // per chunk (offset, size) in 16-B units, consumption order
+  int nchunks;
+  double invN;                       // 1 / N_global
+  const int* skip;
+};
+
+// One weight image segment: a K x O block of W_l (trans = 0: W(o,k) = W_l[k][o],
+// forward) or W_l^T (trans = 1: W(o,k) = W_l[o][k], backward), split into bf16
+// hi/mid/lo planes in 32-deep k-chunks, k permuted to the accumulator pairing,
+// rows swizzled for conflict-free ds_read_b128.  which: 0 = from theta, 1 = tangent.
+struct ChainImgJob {
+  int64_t src_off, dst_off;          // flat-vector offset of W_l; u16 offset in the image
+  int K, O, ldw, trans, kc, otp, which, pad;
+};
+constexpr int kMaxChainJobs = 4 * kMaxLayers;
+struct ChainImgArgs {
+  int n;
+  ChainImgJob job[kMaxChainJobs];
+  unsigned short* img;
+};
+int chain_max_tiles(int max_hidden);   // register tiles for a max hidden width (0: not eligible)
+void launch_fvp_chain(const ChainArgs& a, int otm, hipStream_t s);
+void launch_chain_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
+                      hipStream_t s);
 }  // namespace trpo
