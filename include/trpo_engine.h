@@ -181,6 +181,46 @@ int trpo_profile_enable(trpo_engine* e, int enable);
 int trpo_profile_query(trpo_engine* e, char* buf, int cap);
 int trpo_profile_reset(trpo_engine* e);
 
+/* ==== value-function baseline: class VF (utils.py:48-92) ==================================
+ * Features [obs | action_dist | t/10] (VF._features, utils.py:70-77) -> fully_connected(64, relu)
+ * -> fully_connected(64, relu) -> fully_connected(1) (create_net, utils.py:56-62); fit = 50 steps
+ * of tf.train.AdamOptimizer() on sum((net - y)^2) over the whole batch (utils.py:64-66,79-85);
+ * predict = the net on one path's features (utils.py:87-92).  Parameters are flat in creation
+ * order [W1, b1, W2, b2, W3, b3], W row-major [fan_in][fan_out]. */
+typedef struct trpo_vf trpo_vf;
+/* feat_dim = obs_dim + n_actions + 1; hidden = {64, 64} (utils.py:60-61) or NULL/0 for that default */
+int trpo_vf_create(trpo_vf** out, int feat_dim, const int* hidden, int n_hidden, int64_t max_rows, int device);
+void trpo_vf_destroy(trpo_vf* vf);
+int64_t trpo_vf_num_params(const trpo_vf* vf);
+int trpo_vf_set_params(trpo_vf* vf, const float* flat, int mem);
+int trpo_vf_get_params(trpo_vf* vf, float* flat_out, int mem);
+/* AdamOptimizer(learning_rate, beta1, beta2, epsilon) (defaults 1e-3, 0.9, 0.999, 1e-8); resets the slots */
+int trpo_vf_set_adam(trpo_vf* vf, float lr, float beta1, float beta2, float epsilon);
+/* m = v = 0, beta powers = (beta1, beta2): the state tf.initialize_all_variables() gives (utils.py:66) */
+int trpo_vf_reset_optimizer(trpo_vf* vf);
+/* Adam slots m, v [P] (either may be NULL), beta powers, steps taken */
+int trpo_vf_get_optimizer(trpo_vf* vf, float* m_out, float* v_out, float powers_out[2], int64_t* steps_out,
+                          int mem);
+/* Build the features on the device from a concatenation of paths: obs [n][obs_dim], action_dists
+ * [n][n_actions] f32, episode_starts [n] u8 (1 = first step of a path; NULL = one path).  t counts
+ * steps from each path start.  n_global = rows over all ranks. */
+int trpo_vf_set_features(trpo_vf* vf, int64_t n, int64_t n_global, const float* obs, int obs_dim,
+                         const float* action_dists, int n_actions, const uint8_t* episode_starts, int mem);
+/* ... or take a ready feature matrix [n][feat_dim] f32 */
+int trpo_vf_set_feature_matrix(trpo_vf* vf, int64_t n, int64_t n_global, const float* feat, int mem);
+int trpo_vf_get_feature_matrix(trpo_vf* vf, float* feat_out, int mem);
+/* regression targets = the paths' returns [n] (TRPO_F64 as the reference feeds them, or TRPO_F32) */
+int trpo_vf_set_targets(trpo_vf* vf, const void* returns, int dtype, int mem);
+/* VF.fit's loop body `steps` times (utils.py:84-85; the reference runs 50) */
+int trpo_vf_fit(trpo_vf* vf, int steps);
+/* gradient of sum((net - y)^2) at the current parameters (all ranks) and, if loss_out, that sum */
+int trpo_vf_gradient(trpo_vf* vf, float* grad_out, double* loss_out, int mem);
+/* VF.predict: net on the current features -> out [n] (TRPO_F32 / TRPO_F64) */
+int trpo_vf_predict(trpo_vf* vf, void* out, int dtype, int mem);
+/* multi-GPU: shard rows, all-reduce the [P] gradient (RCCL), or the host test transport */
+int trpo_vf_comm_init(trpo_vf* vf, const uint8_t id[128], int rank, int world);
+int trpo_vf_comm_set_host_allreduce(trpo_vf* vf, trpo_allreduce_cb cb, void* ctx, int rank, int world);
+
 #ifdef __cplusplus
 }
 #endif

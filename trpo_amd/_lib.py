@@ -75,6 +75,25 @@ SIGNATURES = {
     "trpo_profile_enable": (c_int, [c_void_p, c_int]),
     "trpo_profile_query": (c_int, [c_void_p, c_char_p, c_int]),
     "trpo_profile_reset": (c_int, [c_void_p]),
+    # value-function baseline (utils.py:48-92)
+    "trpo_vf_create": (c_int, [POINTER(c_void_p), c_int, POINTER(c_int), c_int, c_int64, c_int]),
+    "trpo_vf_destroy": (None, [c_void_p]),
+    "trpo_vf_num_params": (c_int64, [c_void_p]),
+    "trpo_vf_set_params": (c_int, [c_void_p, c_void_p, c_int]),
+    "trpo_vf_get_params": (c_int, [c_void_p, c_void_p, c_int]),
+    "trpo_vf_set_adam": (c_int, [c_void_p, c_float, c_float, c_float, c_float]),
+    "trpo_vf_reset_optimizer": (c_int, [c_void_p]),
+    "trpo_vf_get_optimizer": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_float), POINTER(c_int64), c_int]),
+    "trpo_vf_set_features": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                     c_int]),
+    "trpo_vf_set_feature_matrix": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int]),
+    "trpo_vf_get_feature_matrix": (c_int, [c_void_p, c_void_p, c_int]),
+    "trpo_vf_set_targets": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "trpo_vf_fit": (c_int, [c_void_p, c_int]),
+    "trpo_vf_gradient": (c_int, [c_void_p, c_void_p, POINTER(c_double), c_int]),
+    "trpo_vf_predict": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "trpo_vf_comm_init": (c_int, [c_void_p, POINTER(c_uint8), c_int, c_int]),
+    "trpo_vf_comm_set_host_allreduce": (c_int, [c_void_p, ALLREDUCE_CB, c_void_p, c_int, c_int]),
 }
 
 

@@ -13,6 +13,7 @@
 //   cg()           utils.py:185-201 with scalars on device and an early-exit flag
 //   update()       trpo_inksci.py:144-158
 #include "../../include/trpo_engine.h"
+#include "abi_util.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -32,61 +33,7 @@
 
 using namespace trpo;
 
-namespace {
-
-thread_local std::string g_last_error;
-
-struct HipError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-struct ArgError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-struct RcclError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-
-#define HIPCHECK(x)                                                                       \
-  do {                                                                                    \
-    hipError_t e_ = (x);                                                                  \
-    if (e_ != hipSuccess)                                                                 \
-      throw HipError(std::string(#x) + " failed: " + hipGetErrorString(e_));              \
-  } while (0)
-#define NCCLCHECK(x)                                                                      \
-  do {                                                                                    \
-    ncclResult_t r_ = (x);                                                                \
-    if (r_ != ncclSuccess) throw RcclError(std::string(#x) + " failed: " + ncclGetErrorString(r_)); \
-  } while (0)
-#define REQUIRE(c, msg)                  \
-  do {                                   \
-    if (!(c)) throw ArgError(msg);       \
-  } while (0)
-
-template <class F>
-int guarded(F&& f) {
-  try {
-    f();
-    return TRPO_OK;
-  } catch (const ArgError& e) {
-    g_last_error = e.what();
-    return TRPO_ERR_ARG;
-  } catch (const RcclError& e) {
-    g_last_error = e.what();
-    return TRPO_ERR_RCCL;
-  } catch (const HipError& e) {
-    g_last_error = e.what();
-    return TRPO_ERR_HIP;
-  } catch (const std::exception& e) {
-    g_last_error = e.what();
-    return TRPO_ERR_STATE;
-  }
-}
-
-inline int pad4(int x) { return (x + 3) & ~3; }
-
-inline void check_launch() { HIPCHECK(hipGetLastError()); }
-
-}  // namespace
+using namespace trpo_abi;
 
 struct trpo_engine {
   int device = 0;
@@ -116,6 +63,7 @@ struct trpo_engine {
   std::vector<uint16_t*> WF3, WB3, WFt3;
   bool w3_valid = false;   // W halves of WF3/WB3 match WF/WB
   float* X = nullptr;
+  float* stage = nullptr;   // staging for host inputs / compact outputs: cap rows of max(pad4(obs), pad4(A), 2) floats
   int* act = nullptr;
   float *adv32 = nullptr, *old = nullptr;
   double *rewards = nullptr, *returns = nullptr, *adv64 = nullptr, *baseline = nullptr;
@@ -259,6 +207,7 @@ struct trpo_engine {
       WFt3.push_back(dalloc<uint16_t>(plane3_f(l) * 3));
     }
     X = dalloc<float>((size_t)cap * wp[0]);
+    stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     act = dalloc<int>(cap);
     adv32 = dalloc<float>(cap);
     old = dalloc<float>((size_t)cap * wp[L]);
@@ -1063,22 +1012,27 @@ int trpo_set_batch(trpo_engine* e, int64_t n, int64_t n_global, const float* sta
         e->copy_in(dst, src, (size_t)n * width * sizeof(float), mem);
         return;
       }
-      float* tmp = nullptr;
-      HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)n * width * sizeof(float), e->stream));
-      e->copy_in(tmp, src, (size_t)n * width * sizeof(float), mem);
-      launch_copy_rows(tmp, n, width, width, dst, ldp, e->stream);
+      // (a stream-ordered hipMallocAsync temporary here lost the pageable host copy on its first
+      // use in the VF runtime; persistent staging avoids the pattern)
+      const float* s = src;
+      if (mem != TRPO_MEM_DEVICE) {
+        e->copy_in(e->stage, src, (size_t)n * width * sizeof(float), mem);
+        s = e->stage;
+      }
+      launch_copy_rows(s, n, width, width, dst, ldp, e->stream);
       check_launch();
-      HIPCHECK(hipFreeAsync(tmp, e->stream));
+      HIPCHECK(hipStreamSynchronize(e->stream));
     };
     stage(states, obs, e->wp[0], e->X);
     stage(old_dist, A, e->wp[e->L], e->old);
-    int64_t* tmp = nullptr;
-    HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)n * sizeof(int64_t), e->stream));
-    e->copy_in(tmp, actions, (size_t)n * sizeof(int64_t), mem);
+    const int64_t* acts = actions;
+    if (mem != TRPO_MEM_DEVICE) {
+      e->copy_in(e->stage, actions, (size_t)n * sizeof(int64_t), mem);
+      acts = reinterpret_cast<const int64_t*>(e->stage);
+    }
     HIPCHECK(hipMemsetAsync(e->dbad, 0, sizeof(int), e->stream));
-    launch_i64_to_i32(tmp, e->act, n, e->dbad, A, e->stream);
+    launch_i64_to_i32(acts, e->act, n, e->dbad, A, e->stream);
     check_launch();
-    HIPCHECK(hipFreeAsync(tmp, e->stream));
     int bad = 0;
     e->copy_out(&bad, e->dbad, sizeof(int), TRPO_MEM_HOST);
     REQUIRE(!bad, "action index out of range [0, n_actions)");
@@ -1142,12 +1096,10 @@ int trpo_action_dist(trpo_engine* e, float* out, int mem) {
     e->use();
     e->prepare();
     const int A = e->w[e->L];
-    float* tmp = nullptr;
-    HIPCHECK(hipMallocAsync((void**)&tmp, (size_t)e->n * A * sizeof(float), e->stream));
-    launch_copy_rows(e->Pm, e->n, A, e->wp[e->L], tmp, A, e->stream);
+    float* dst = mem == TRPO_MEM_DEVICE ? out : e->stage;
+    launch_copy_rows(e->Pm, e->n, A, e->wp[e->L], dst, A, e->stream);
     check_launch();
-    e->copy_out(out, tmp, (size_t)e->n * A * sizeof(float), mem);
-    HIPCHECK(hipFreeAsync(tmp, e->stream));
+    if (mem != TRPO_MEM_DEVICE) e->copy_out(out, e->stage, (size_t)e->n * A * sizeof(float), mem);
     HIPCHECK(hipStreamSynchronize(e->stream));
   });
 }

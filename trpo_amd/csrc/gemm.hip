@@ -80,6 +80,10 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
     e.out0[idx] = real ? v * one_minus_sq(e.H[idx]) : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
     e.out0[idx] = real ? fmaf(e.E[idx], e.RH[idx], v * one_minus_sq(e.H[idx])) : 0.0f;
+  } else if constexpr (EPI == (int)RowEpi::kRelu) {
+    e.out0[idx] = real ? fmaxf(v + e.bias[col], 0.0f) : 0.0f;
+  } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
+    e.out0[idx] = (real && e.H[idx] > 0.0f) ? v : 0.0f;
   }
 }
 
@@ -103,6 +107,10 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
     o0 = v * one_minus_sq(e.H[idx]);
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
     o0 = fmaf(e.E[idx], e.RH[idx], v * one_minus_sq(e.H[idx]));
+  } else if constexpr (EPI == (int)RowEpi::kRelu) {
+    o0 = fmaxf(v + bv, 0.0f);
+  } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
+    o0 = e.H[idx] > 0.0f ? v : 0.0f;
   }
 }
 template <int EPI>
@@ -211,7 +219,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int M = args.M;
   const RowEpiArgs& e = args.ea;
-  if constexpr (EPI >= (int)RowEpi::kPrepHead) {
+  if constexpr (epi_is_head(EPI)) {
     static_assert(WN == 1 && TN == 1, "row-wise head epilogue needs the whole row in one wave half");
     const int col = n0 + lr;
 #pragma unroll
@@ -237,7 +245,8 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
         return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
       };
       constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
-                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd;
+                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd ||
+                              EPI == (int)RowEpi::kReluBwd;
       constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
       constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd;
       // descriptors of operands an epilogue does not use alias out0 and are never touched
@@ -257,7 +266,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
       for (int tn = 0; tn < TN; ++tn) {
         const int col = n0 + wn * TN * 32 + tn * 32 + lr;
         float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden)
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu)
           bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
         const int vo = vbase + tn * 128;
 #pragma unroll
@@ -277,6 +286,10 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
               o1[r] = -2.0f * v * h;
             } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
               o0[r] = v * one_minus_sq(ld(rH, vo, so));
+            } else if constexpr (EPI == (int)RowEpi::kRelu) {
+              o0[r] = fmaxf(v + bv, 0.0f);
+            } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
+              o0[r] = ld(rH, vo, so) > 0.0f ? v : 0.0f;
             } else {
               o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
             }
@@ -298,7 +311,8 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
         const bool colv = col < args.Npad;
         const int colc = colv ? col : 0;
         float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden) bv = e.bias[real ? col : 0];
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu)
+          bv = e.bias[real ? col : 0];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -1092,7 +1106,7 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
 
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
-  if constexpr (EPI >= (int)RowEpi::kPrepHead) {
+  if constexpr (epi_is_head(EPI)) {
     if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
     if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
@@ -1143,7 +1157,7 @@ void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
 }  // namespace
 
 bool rowgemm_uses_split(int Npad, RowEpi epi) {
-  return g_options.split_mfma != 0 && Npad > 128 && (int)epi < (int)RowEpi::kPrepHead;
+  return g_options.split_mfma != 0 && Npad > 128 && !epi_is_head((int)epi);
 }
 
 void launch_split_b(const SplitArgs& a, const int* skip, hipStream_t s) {
@@ -1169,6 +1183,8 @@ void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
     case RowEpi::kPrepHead: launch_row_epi<(int)RowEpi::kPrepHead>(a, s); break;
     case RowEpi::kLossHead: launch_row_epi<(int)RowEpi::kLossHead>(a, s); break;
     case RowEpi::kRHead: launch_row_epi<(int)RowEpi::kRHead>(a, s); break;
+    case RowEpi::kRelu: launch_row_epi<(int)RowEpi::kRelu>(a, s); break;
+    case RowEpi::kReluBwd: launch_row_epi<(int)RowEpi::kReluBwd>(a, s); break;
   }
 }
 

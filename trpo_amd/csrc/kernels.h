@@ -46,7 +46,11 @@ enum class RowEpi : int {
   kPrepHead = 5,  // softmax head: P, D_L, DS_L, row loss terms  (prepare)
   kLossHead = 6,  // softmax head: row loss terms only           (line search)
   kRHead = 7,     // R-softmax head: RD_L                        (FVP)
+  kRelu = 8,      // out = max(acc + bias, 0)                    (VF forward, utils.py:60-61)
+  kReluBwd = 9,   // out = acc * (H > 0), H = the ReLU output    (VF backward)
 };
+// the row-wise softmax heads (one output row per 32-lane wave half)
+constexpr bool epi_is_head(int e) { return e >= (int)RowEpi::kPrepHead && e <= (int)RowEpi::kRHead; }
 
 struct RowEpiArgs {
   const float* bias;   // [N] (kTanh, kRHidden, heads)
@@ -214,6 +218,7 @@ void launch_ls_finalize(const float* prev, const float* fullstep, float* theta, 
 void launch_axpby(float* y, const float* x, float alpha, float beta, int64_t n, hipStream_t s);  // y = alpha*x + beta*y
 void launch_scale_copy(const float* x, float* y, float alpha, int64_t n, hipStream_t s);          // y = alpha*x
 void launch_i64_to_i32(const int64_t* src, int* dst, int64_t n, int* bad, int hi, hipStream_t s);
+void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s);
 void launch_copy_rows(const float* src, int64_t n, int w, int ld_src, float* dst, int ld_dst, hipStream_t s);
 
 // ---------------------------------------------------------------------------
@@ -335,4 +340,41 @@ int chain_max_tiles(int max_hidden);   // register tiles for a max hidden width 
 void launch_fvp_chain(const ChainArgs& a, int otm, hipStream_t s);
 void launch_chain_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
                       hipStream_t s);
+}  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Value-function baseline (vf.hip), utils.py:48-92
+// ---------------------------------------------------------------------------
+size_t vf_pos_workspace_bytes(int64_t n);
+// feat [n][Fp] = [obs | dist | f32(t/10)] with t the step index within each path
+// (starts[r] = 1 opens a path; starts may be NULL: one path); lastpos [n] scratch
+void launch_vf_features(const float* obs, int obs_dim, int ld_obs, const float* dist, int A, int ld_dist,
+                        const uint8_t* starts, int64_t n, int64_t* lastpos, void* ws, float* feat, int Fp,
+                        hipStream_t s);
+struct VFPackArgs {
+  int F, H1, H2, H1p, H2p;
+  int64_t offW1, offW2;   // flat offsets of W1 [F][H1], W2 [H1][H2]
+  float* W1p;             // [Fp][H1p]
+  float* W2p;             // [H1p][H2p]
+  float* W2T;             // [H2p][H1p]
+};
+void launch_vf_pack(const VFPackArgs& a, const float* theta, hipStream_t s);
+struct VFHeadArgs {
+  int64_t n;
+  int H2, H2p;
+  const float* Z2;        // [n][H2p]
+  const float* w3;        // [H2]
+  const float* b3;        // [1]
+  int train;
+  const float* y;         // [n]            train
+  float* dout;            // [n][4]         train: col 0 = d(loss)/d(net)
+  float* dZ2;             // [n][H2p]       train
+  double* loss_rows;      // [n]            train: (net - y)^2
+  float* out32;           // [n]            predict (if out64 == NULL)
+  double* out64;          // [n]            predict
+};
+void launch_vf_head(const VFHeadArgs& a, hipStream_t s);
+void launch_adam(float* var, const float* g, float* m, float* v, int64_t n, float alpha, float b1, float b2, float eps,
+                 hipStream_t s);
 }  // namespace trpo

@@ -331,6 +331,11 @@ __global__ void copy_rows_kernel(const float* src, int64_t n, int w, int ld_src,
   }
 }
 
+__global__ void f64_to_f32_kernel(const double* src, float* dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (float)src[i];
+}
+
 inline int grid_for(int64_t n, int threads = 256, int cap = 4096) {
   int64_t g = (n + threads - 1) / threads;
   if (g < 1) g = 1;
@@ -451,6 +456,10 @@ void launch_scale_copy(const float* x, float* y, float alpha, int64_t n, hipStre
 
 void launch_i64_to_i32(const int64_t* src, int* dst, int64_t n, int* bad, int hi, hipStream_t s) {
   hipLaunchKernelGGL(i64_to_i32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n, bad, hi);
+}
+
+void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(f64_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
 }
 
 void launch_copy_rows(const float* src, int64_t n, int w, int ld_src, float* dst, int ld_dst,
