@@ -181,6 +181,47 @@ int trpo_profile_enable(trpo_engine* e, int enable);
 int trpo_profile_query(trpo_engine* e, char* buf, int cap);
 int trpo_profile_reset(trpo_engine* e);
 
+/* ==== sampling and rollouts (trpo_inksci.py:76-87, utils.py:18-45,95-105) ======================
+ * The reference steps one gym CartPole-v0 env and calls agent.act once per step (a 1-row
+ * session.run + cat_sample).  Here n_envs CartPole-v0 instances (gym's classic_control/cartpole.py
+ * restated in float64; gym is not vendored) run on the GPU, one wave each, under the engine's
+ * current policy.  Every environment collects whole episodes until its own step count reaches
+ * ceil(n_timesteps / n_envs) -- utils.py:23-44's stopping rule per environment (n_envs = 1 is the
+ * reference's loop) -- and the episodes are concatenated in environment order. */
+typedef struct trpo_rollout_params {
+  int n_envs;                /* parallel environments (1) */
+  int max_pathlength;        /* config["max_steps"] = 1000 (trpo_inksci.py:17; utils.py:28) */
+  int64_t n_timesteps;       /* config["episodes_per_roll"] = 1000 (trpo_inksci.py:17; utils.py:23) */
+  int train;                 /* 1: cat_sample; 0: argmax (trpo_inksci.py:79-83) */
+  int time_limit;            /* CartPole-v0's TimeLimit: 200 steps */
+  uint64_t seed;             /* Philox stream: action uniforms and env.reset draws */
+  /* optional injected uniforms (tests): reset [n_envs][max_episodes_per_env][4] in [0,1) and
+   * cat_sample [n_envs][ceil(n_timesteps/n_envs) + min(max_pathlength, time_limit) - 1] */
+  const double* reset_uniforms;
+  const double* action_uniforms;
+  int max_episodes_per_env;
+  int mem;                   /* where the injected arrays live */
+} trpo_rollout_params;
+void trpo_default_rollout_params(trpo_rollout_params* p);
+/* run the rollout; returns the total steps N and the number of paths */
+int trpo_rollout_cartpole(trpo_engine* e, const trpo_rollout_params* p, int64_t* n_steps_out, int64_t* n_paths_out);
+/* the concatenated paths (utils.py:36-39): obs [N][4] f64, actions [N] i64, action_dists [N][A] f32,
+ * rewards [N] f64, episode_starts [N] u8, and the cat_sample uniform of every step; any may be NULL */
+int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* action_dists, double* rewards,
+                       uint8_t* episode_starts, double* uniforms, int mem);
+/* the rollout becomes the feed on the device (trpo_inksci.py:108-112,119-122): states, actions,
+ * oldaction_dist, rewards and path starts, with no host round trip; baseline cleared */
+int trpo_rollout_to_batch(trpo_engine* e, int64_t n_global);
+/* agent.act on n states [n][obs_dim] f32 (trpo_inksci.py:76-87): action_dist at the current
+ * parameters and cat_sample against `uniforms` [n] (train = 1) or argmax (train = 0) */
+int trpo_act(trpo_engine* e, const float* states, int64_t n, const double* uniforms, int train, int64_t* actions_out,
+             float* dists_out, int mem);
+/* cat_sample(prob_nk) (utils.py:95-105) with the uniforms given: engine-free, current device */
+int trpo_cat_sample(const float* prob, int64_t n, int k, const double* uniforms, int64_t* out, int mem);
+/* one CartPole-v0 step per row (state [n][4] f64, action [n] i64); done = termination (not the TimeLimit) */
+int trpo_cartpole_step(const double* state, const int64_t* action, int64_t n, double* state_out, double* reward,
+                       uint8_t* done, int mem);
+
 /* ==== value-function baseline: class VF (utils.py:48-92) ==================================
  * Features [obs | action_dist | t/10] (VF._features, utils.py:70-77) -> fully_connected(64, relu)
  * -> fully_connected(64, relu) -> fully_connected(1) (create_net, utils.py:56-62); fit = 50 steps

@@ -199,8 +199,64 @@ def gen_update(U, name, spec, n, seed, max_kl=0.01, steady=True, perturb=0.0,
           f"kl={losses_after[1]:.4g} fvp-crosscheck={rel:.2e}")
 
 
-def main():
+def gen_rollout(U):
+    """The reference's own ``rollout`` (utils.py:18-45) and ``cat_sample`` (utils.py:95-105) driving
+    the CartPole-v0 restatement and a float32 policy agent (oracle/cartpole_oracle.py).  The
+    uniforms both RNGs produced are recorded, so the device rollout can be fed the same draws."""
+    from oracle.cartpole_oracle import CartPoleV0, OracleAgent
+    spec = O.PolicySpec(4, [64], 2)
+    out = {}
+    for tag, seed, n_timesteps, train in (("a", 11, 1000, True), ("b", 12, 450, True), ("c", 13, 300, False)):
+        rng = np.random.RandomState(seed)
+        theta = np.concatenate([np.concatenate([rng.uniform(-np.sqrt(6 / (a + b)), np.sqrt(6 / (a + b)), a * b),
+                                                0.3 * rng.standard_normal(b)])
+                                for a, b in zip(spec.widths[:-1], spec.widths[1:])]).astype(np.float32)
+        env = CartPoleV0(seed=100 + seed)
+        agent = OracleAgent(theta, spec.widths, U.cat_sample, train=train)
+        np.random.seed(200 + seed)
+        paths = U.rollout(env, agent, 1000, n_timesteps)
+        n = sum(len(p["rewards"]) for p in paths)
+        starts = np.concatenate([np.r_[1, np.zeros(len(p["rewards"]) - 1)] for p in paths]).astype(np.uint8)
+        out[tag + "_theta"] = theta
+        out[tag + "_n_timesteps"] = np.int64(n_timesteps)
+        out[tag + "_train"] = np.bool_(train)
+        out[tag + "_obs"] = np.concatenate([p["obs"] for p in paths]).astype(np.float64)
+        out[tag + "_actions"] = np.concatenate([p["actions"] for p in paths]).astype(np.int64)
+        out[tag + "_action_dists"] = np.concatenate([p["action_dists"] for p in paths]).astype(np.float32)
+        out[tag + "_rewards"] = np.concatenate([p["rewards"] for p in paths]).astype(np.float64)
+        out[tag + "_starts"] = starts
+        # the draws: np.random.rand(1) per act() in training, 4 per env.reset()
+        out[tag + "_act_uniforms"] = np.random.RandomState(200 + seed).random_sample(n) if train else np.zeros(n)
+        out[tag + "_reset_uniforms"] = np.random.RandomState(100 + seed).random_sample(4 * len(paths))
+        print(f"  rollout {tag}: {len(paths)} paths, {n} steps")
+    rng = np.random.RandomState(5)
+    prob = rng.dirichlet(np.ones(7), 400).astype(np.float32)
+    prob[:50] = np.float32(1.0 / 7)                       # cumsum can end below r (out stays 0)
+    r = np.random.RandomState(9).random_sample(400)
+    prob[:10] *= np.float32(0.999)                        # cumsum ends at 0.999 < r = 0.9995:
+    r[:10] = 0.9995                                       # the reference's zeros-init fallback
+    # cat_sample draws np.random.rand(N) itself: call it per row with np.random.rand
+    # temporarily returning r[i]
+    vals = []
+    orig = U.np.random.rand
+    try:
+        for i in range(400):
+            U.np.random.rand = (lambda *a, _v=r[i]: np.array([_v]))
+            vals.append(int(U.cat_sample(prob[i:i + 1])[0]))
+    finally:
+        U.np.random.rand = orig
+    out["cat_prob"] = prob
+    out["cat_r"] = r
+    out["cat_out"] = np.array(vals, np.int64)
+    _save("rollout.npz", **out)
+
+
+def main(only=None):
     U = load_reference_utils()
+    if only == "rollout":
+        gen_rollout(U)
+        return
+    gen_rollout(U)
     gen_discount(U)
     gen_cg(U)
     gen_linesearch(U)
@@ -215,4 +271,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

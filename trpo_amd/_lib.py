@@ -36,6 +36,12 @@ class UpdateStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad"}
 
 
+class RolloutParams(ctypes.Structure):
+    _fields_ = [("n_envs", c_int), ("max_pathlength", c_int), ("n_timesteps", c_int64), ("train", c_int),
+                ("time_limit", c_int), ("seed", ctypes.c_uint64), ("reset_uniforms", c_void_p),
+                ("action_uniforms", c_void_p), ("max_episodes_per_env", c_int), ("mem", c_int)]
+
+
 FAX_CB = CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p)
 ALLREDUCE_CB = CFUNCTYPE(c_int, c_void_p, c_int64, c_int, c_void_p)
 F32, F64 = 0, 1
@@ -75,6 +81,14 @@ SIGNATURES = {
     "trpo_profile_enable": (c_int, [c_void_p, c_int]),
     "trpo_profile_query": (c_int, [c_void_p, c_char_p, c_int]),
     "trpo_profile_reset": (c_int, [c_void_p]),
+    # sampling / rollouts (trpo_inksci.py:76-87, utils.py:18-45,95-105)
+    "trpo_default_rollout_params": (None, [POINTER(RolloutParams)]),
+    "trpo_rollout_cartpole": (c_int, [c_void_p, POINTER(RolloutParams), POINTER(c_int64), POINTER(c_int64)]),
+    "trpo_rollout_fetch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "trpo_rollout_to_batch": (c_int, [c_void_p, c_int64]),
+    "trpo_act": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int]),
+    "trpo_cat_sample": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int]),
+    "trpo_cartpole_step": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int]),
     # value-function baseline (utils.py:48-92)
     "trpo_vf_create": (c_int, [POINTER(c_void_p), c_int, POINTER(c_int), c_int, c_int64, c_int]),
     "trpo_vf_destroy": (None, [c_void_p]),

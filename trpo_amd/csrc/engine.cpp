@@ -29,6 +29,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 using namespace trpo;
@@ -99,6 +100,25 @@ struct trpo_engine {
   bool use_chain() const {
     return chain_otm > 0 && (g_options.chain >= 2 || (g_options.chain == 1 && chain_otm <= 8));
   }
+
+  // rollout (rollout.hip): per-environment regions, reallocated when a rollout needs more
+  struct RollBufs {
+    std::vector<void*> mem;
+    int64_t rows = 0;      // capacity in region rows
+    int envs = 0;
+    double* obs = nullptr;
+    int64_t* actions = nullptr;
+    float* dist = nullptr;
+    double* rewards = nullptr;
+    uint8_t* starts = nullptr;
+    double* uniforms = nullptr;
+    int64_t *counts = nullptr, *episodes = nullptr, *offsets = nullptr;
+    double *reset_u = nullptr, *act_u = nullptr;
+    int64_t reset_u_n = 0, act_u_n = 0;
+  } roll;
+  RolloutArgs roll_args{};
+  int64_t roll_n = 0, roll_paths = 0, roll_maxcount = 0;
+  bool roll_valid = false;
 
   // profiling
   bool prof = false;
@@ -312,6 +332,121 @@ struct trpo_engine {
     chain_otm = otm;
   }
 
+  PolicyShape policy_shape() const {
+    PolicyShape ps{};
+    ps.L = L;
+    for (int l = 0; l <= L; ++l) ps.w[l] = w[l];
+    for (int l = 0; l < L; ++l) {
+      ps.offW[l] = offW[l];
+      ps.offb[l] = offb[l];
+    }
+    return ps;
+  }
+  int max_width() const {
+    int m = 1;
+    for (int l = 0; l <= L; ++l) m = std::max(m, w[l]);
+    return m;
+  }
+
+  template <class T>
+  T* ralloc(size_t count) {
+    void* ptr = nullptr;
+    HIPCHECK(hipMalloc(&ptr, std::max<size_t>(count * sizeof(T), 16)));
+    roll.mem.push_back(ptr);
+    return static_cast<T*>(ptr);
+  }
+
+  // rollout (utils.py:18-45) of n_envs CartPole-v0 instances under the current policy
+  void rollout(const trpo_rollout_params& p) {
+    REQUIRE(p.n_envs >= 1 && p.n_envs <= (1 << 20), "n_envs out of range");
+    REQUIRE(p.n_timesteps >= 1 && p.max_pathlength >= 1 && p.time_limit >= 1, "bad rollout lengths");
+    REQUIRE(w[0] == 4 && w[L] == 2, "CartPole-v0 needs obs_dim 4 and 2 actions");
+    const int ep_max = std::min(p.max_pathlength, p.time_limit);
+    const int64_t budget = (p.n_timesteps + p.n_envs - 1) / p.n_envs;
+    const int64_t env_cap = budget + ep_max - 1;
+    const int64_t rows = env_cap * p.n_envs;
+    REQUIRE(rows <= (int64_t(1) << 34), "rollout too large");
+    if (rows > roll.rows || p.n_envs > roll.envs) {
+      for (void* ptr : roll.mem) HIPCHECK(hipFree(ptr));
+      roll = RollBufs{};
+      roll.rows = rows;
+      roll.envs = p.n_envs;
+      roll.obs = ralloc<double>((size_t)rows * 4);
+      roll.actions = ralloc<int64_t>(rows);
+      roll.dist = ralloc<float>((size_t)rows * 2);
+      roll.rewards = ralloc<double>(rows);
+      roll.starts = ralloc<uint8_t>(rows);
+      roll.uniforms = ralloc<double>(rows);
+      roll.counts = ralloc<int64_t>(p.n_envs);
+      roll.episodes = ralloc<int64_t>(p.n_envs);
+      roll.offsets = ralloc<int64_t>(p.n_envs);
+    }
+    RolloutArgs a{};
+    a.ps = policy_shape();
+    a.theta = theta;
+    a.maxw = max_width();
+    a.n_envs = p.n_envs;
+    a.max_pathlength = p.max_pathlength;
+    a.time_limit = p.time_limit;
+    a.train = p.train;
+    a.budget = budget;
+    a.env_cap = env_cap;
+    a.max_episodes = p.max_episodes_per_env;
+    a.seed = p.seed;
+    // optional injected uniforms (tests): reset [n_envs][max_episodes][4], act [n_envs][env_cap]
+    auto stage_u = [&](const double* src, int64_t count, double*& buf, int64_t& cap_n) -> const double* {
+      if (!src) return nullptr;
+      if (p.mem == TRPO_MEM_DEVICE) return src;
+      if (count > cap_n) {
+        buf = ralloc<double>(count);
+        cap_n = count;
+      }
+      copy_in(buf, src, (size_t)count * sizeof(double), TRPO_MEM_HOST);
+      return buf;
+    };
+    if (p.reset_uniforms) REQUIRE(p.max_episodes_per_env >= 1, "max_episodes_per_env required with reset_uniforms");
+    a.reset_u = stage_u(p.reset_uniforms, (int64_t)p.n_envs * std::max(1, p.max_episodes_per_env) * 4, roll.reset_u,
+                        roll.reset_u_n);
+    a.act_u = stage_u(p.action_uniforms, rows, roll.act_u, roll.act_u_n);
+    if (a.reset_u) {
+      // every episode an environment can start must have its uniforms
+      REQUIRE((int64_t)p.max_episodes_per_env >= budget, "max_episodes_per_env must be >= ceil(n_timesteps/n_envs)");
+    }
+    a.obs = roll.obs;
+    a.actions = roll.actions;
+    a.dist = roll.dist;
+    a.rewards = roll.rewards;
+    a.starts = roll.starts;
+    a.uniforms_out = roll.uniforms;
+    a.counts = roll.counts;
+    a.episodes = roll.episodes;
+    launch_rollout(a, stream);
+    check_launch();
+    std::vector<int64_t> counts(p.n_envs), offs(p.n_envs);
+    copy_out(counts.data(), roll.counts, counts.size() * sizeof(int64_t), TRPO_MEM_HOST);
+    int64_t tot = 0, mx = 0;
+    for (int i = 0; i < p.n_envs; ++i) {
+      offs[i] = tot;
+      tot += counts[i];
+      mx = std::max(mx, counts[i]);
+    }
+    copy_in(roll.offsets, offs.data(), offs.size() * sizeof(int64_t), TRPO_MEM_HOST);
+    std::vector<int64_t> eps(p.n_envs);
+    copy_out(eps.data(), roll.episodes, eps.size() * sizeof(int64_t), TRPO_MEM_HOST);
+    roll_args = a;
+    roll_n = tot;
+    roll_maxcount = mx;
+    roll_paths = 0;
+    for (int64_t x : eps) roll_paths += x;
+    roll_valid = true;
+  }
+
+  void rollout_compact(const RolloutOut& o) {
+    REQUIRE(roll_valid, "no rollout to fetch");
+    launch_rollout_compact(roll_args, roll.offsets, o, roll_maxcount, stream);
+    check_launch();
+  }
+
   void release() {
     if (device >= 0) (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
@@ -322,6 +457,8 @@ struct trpo_engine {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (void* ptr : allocs) (void)hipFree(ptr);
     allocs.clear();
+    for (void* ptr : roll.mem) (void)hipFree(ptr);
+    roll.mem.clear();
     if (hsc) (void)hipHostFree(hsc);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1279,6 +1416,217 @@ int trpo_device_count(int* out) {
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     (void)hipGetLastError();
     *out = n;
+  });
+}
+
+void trpo_default_rollout_params(trpo_rollout_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof *p);
+  p->n_envs = 1;
+  p->max_pathlength = 1000;    // config["max_steps"] (trpo_inksci.py:17)
+  p->n_timesteps = 1000;       // config["episodes_per_roll"] (trpo_inksci.py:17, used as a step budget)
+  p->train = 1;
+  p->time_limit = 200;         // CartPole-v0 TimeLimit
+  p->seed = 1;
+  p->mem = TRPO_MEM_HOST;
+}
+
+int trpo_rollout_cartpole(trpo_engine* e, const trpo_rollout_params* p, int64_t* n_steps_out, int64_t* n_paths_out) {
+  return guarded([&] {
+    REQUIRE(e && p, "NULL argument");
+    e->use();
+    e->rollout(*p);
+    if (n_steps_out) *n_steps_out = e->roll_n;
+    if (n_paths_out) *n_paths_out = e->roll_paths;
+  });
+}
+
+int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* action_dists, double* rewards,
+                       uint8_t* episode_starts, double* uniforms, int mem) {
+  return guarded([&] {
+    REQUIRE(e, "NULL argument");
+    REQUIRE(e->roll_valid, "no rollout to fetch");
+    e->use();
+    const int64_t N = e->roll_n;
+    const int obs_dim = e->w[0], A = e->w[e->L];
+    RolloutOut o{};
+    std::vector<void*> tmps;
+    auto dst = [&](auto* user, size_t elems) {
+      using T = std::remove_pointer_t<decltype(user)>;
+      if (!user || mem == TRPO_MEM_DEVICE) return user;
+      void* ptr = nullptr;
+      HIPCHECK(hipMalloc(&ptr, std::max<size_t>(elems * sizeof(T), 16)));
+      tmps.push_back(ptr);
+      return static_cast<T*>(ptr);
+    };
+    o.obs64 = dst(obs, (size_t)N * obs_dim);
+    o.actions64 = dst(actions, (size_t)N);
+    o.dist = dst(action_dists, (size_t)N * A);
+    o.rewards = dst(rewards, (size_t)N);
+    o.starts = dst(episode_starts, (size_t)N);
+    o.uniforms = dst(uniforms, (size_t)N);
+    try {
+      e->rollout_compact(o);
+      if (mem != TRPO_MEM_DEVICE) {
+        if (obs) e->copy_out(obs, o.obs64, (size_t)N * obs_dim * sizeof(double), mem);
+        if (actions) e->copy_out(actions, o.actions64, (size_t)N * sizeof(int64_t), mem);
+        if (action_dists) e->copy_out(action_dists, o.dist, (size_t)N * A * sizeof(float), mem);
+        if (rewards) e->copy_out(rewards, o.rewards, (size_t)N * sizeof(double), mem);
+        if (episode_starts) e->copy_out(episode_starts, o.starts, (size_t)N, mem);
+        if (uniforms) e->copy_out(uniforms, o.uniforms, (size_t)N * sizeof(double), mem);
+      }
+      HIPCHECK(hipStreamSynchronize(e->stream));
+    } catch (...) {
+      for (void* t : tmps) (void)hipFree(t);
+      throw;
+    }
+    for (void* t : tmps) HIPCHECK(hipFree(t));
+  });
+}
+
+int trpo_rollout_to_batch(trpo_engine* e, int64_t n_global) {
+  return guarded([&] {
+    REQUIRE(e, "NULL argument");
+    REQUIRE(e->roll_valid, "no rollout to load");
+    const int64_t N = e->roll_n;
+    REQUIRE(N <= e->cap, "rollout has more steps than max_rows");
+    REQUIRE(n_global >= N, "n_global must be >= the rollout's steps");
+    e->use();
+    RolloutOut o{};
+    o.X = e->X;
+    o.ldx = e->wp[0];
+    o.old = e->old;
+    o.ld_old = e->wp[e->L];
+    o.act32 = e->act;
+    o.rewards = e->rewards;
+    o.starts = e->starts;
+    e->rollout_compact(o);
+    e->n = N;
+    e->n_global = n_global;
+    e->set_splits();
+    e->prepared = false;
+    e->have_rewards = true;
+    e->have_baseline = false;
+    HIPCHECK(hipStreamSynchronize(e->stream));
+  });
+}
+
+int trpo_act(trpo_engine* e, const float* states, int64_t n, const double* uniforms, int train, int64_t* actions_out,
+             float* dists_out, int mem) {
+  return guarded([&] {
+    REQUIRE(e && states && n >= 0, "bad argument");
+    REQUIRE(!train || uniforms, "train = 1 needs uniforms (cat_sample's np.random.rand)");
+    e->use();
+    if (n == 0) return;
+    const int obs = e->w[0], A = e->w[e->L];
+    const float* s = states;
+    const double* r = uniforms;
+    int64_t* ao = actions_out;
+    float* dout = dists_out;
+    std::vector<void*> tmps;
+    auto dev = [&](size_t bytes) {
+      void* ptr = nullptr;
+      HIPCHECK(hipMalloc(&ptr, std::max<size_t>(bytes, 16)));
+      tmps.push_back(ptr);
+      return ptr;
+    };
+    try {
+      if (mem != TRPO_MEM_DEVICE) {
+        float* ds = static_cast<float*>(dev((size_t)n * obs * sizeof(float)));
+        e->copy_in(ds, states, (size_t)n * obs * sizeof(float), mem);
+        s = ds;
+        if (uniforms) {
+          double* dr = static_cast<double*>(dev((size_t)n * sizeof(double)));
+          e->copy_in(dr, uniforms, (size_t)n * sizeof(double), mem);
+          r = dr;
+        }
+        if (actions_out) ao = static_cast<int64_t*>(dev((size_t)n * sizeof(int64_t)));
+        if (dists_out) dout = static_cast<float*>(dev((size_t)n * A * sizeof(float)));
+      }
+      launch_act(e->policy_shape(), e->theta, e->max_width(), s, n, r, train, ao, dout, e->stream);
+      check_launch();
+      if (mem != TRPO_MEM_DEVICE) {
+        if (actions_out) e->copy_out(actions_out, ao, (size_t)n * sizeof(int64_t), mem);
+        if (dists_out) e->copy_out(dists_out, dout, (size_t)n * A * sizeof(float), mem);
+      }
+      HIPCHECK(hipStreamSynchronize(e->stream));
+    } catch (...) {
+      for (void* t : tmps) (void)hipFree(t);
+      throw;
+    }
+    for (void* t : tmps) HIPCHECK(hipFree(t));
+  });
+}
+
+namespace {
+// engine-free kernels on the current device: stage host arrays in plain hipMalloc buffers
+struct Scratch {
+  std::vector<void*> p;
+  void* get(size_t bytes) {
+    void* ptr = nullptr;
+    HIPCHECK(hipMalloc(&ptr, std::max<size_t>(bytes, 16)));
+    p.push_back(ptr);
+    return ptr;
+  }
+  ~Scratch() {
+    for (void* x : p) (void)hipFree(x);
+  }
+};
+}  // namespace
+
+int trpo_cat_sample(const float* prob, int64_t n, int k, const double* r, int64_t* out, int mem) {
+  return guarded([&] {
+    REQUIRE(prob && r && out && n >= 0 && k >= 1, "bad argument");
+    if (n == 0) return;
+    Scratch sc;
+    const float* dp = prob;
+    const double* dr = r;
+    int64_t* dout = out;
+    if (mem != TRPO_MEM_DEVICE) {
+      float* a = static_cast<float*>(sc.get((size_t)n * k * sizeof(float)));
+      double* b = static_cast<double*>(sc.get((size_t)n * sizeof(double)));
+      HIPCHECK(hipMemcpy(a, prob, (size_t)n * k * sizeof(float), hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(b, r, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+      dp = a;
+      dr = b;
+      dout = static_cast<int64_t*>(sc.get((size_t)n * sizeof(int64_t)));
+    }
+    launch_cat_sample(dp, n, k, dr, dout, nullptr);
+    check_launch();
+    if (mem != TRPO_MEM_DEVICE) HIPCHECK(hipMemcpy(out, dout, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHECK(hipDeviceSynchronize());
+  });
+}
+
+int trpo_cartpole_step(const double* state, const int64_t* action, int64_t n, double* state_out, double* reward,
+                       uint8_t* done, int mem) {
+  return guarded([&] {
+    REQUIRE(state && action && state_out && n >= 0, "bad argument");
+    if (n == 0) return;
+    Scratch sc;
+    const double* ds = state;
+    const int64_t* da = action;
+    double *dso = state_out, *dr = reward;
+    uint8_t* dd = done;
+    if (mem != TRPO_MEM_DEVICE) {
+      double* a = static_cast<double*>(sc.get((size_t)n * 4 * sizeof(double)));
+      int64_t* b = static_cast<int64_t*>(sc.get((size_t)n * sizeof(int64_t)));
+      HIPCHECK(hipMemcpy(a, state, (size_t)n * 4 * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(b, action, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice));
+      ds = a;
+      da = b;
+      dso = static_cast<double*>(sc.get((size_t)n * 4 * sizeof(double)));
+      dr = reward ? static_cast<double*>(sc.get((size_t)n * sizeof(double))) : nullptr;
+      dd = done ? static_cast<uint8_t*>(sc.get((size_t)n)) : nullptr;
+    }
+    launch_cartpole_step(ds, da, n, dso, dr, dd, nullptr);
+    check_launch();
+    if (mem != TRPO_MEM_DEVICE) {
+      HIPCHECK(hipMemcpy(state_out, dso, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+      if (reward) HIPCHECK(hipMemcpy(reward, dr, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+      if (done) HIPCHECK(hipMemcpy(done, dd, (size_t)n, hipMemcpyDeviceToHost));
+    }
+    HIPCHECK(hipDeviceSynchronize());
   });
 }
 

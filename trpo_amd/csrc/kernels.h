@@ -378,3 +378,58 @@ void launch_vf_head(const VFHeadArgs& a, hipStream_t s);
 void launch_adam(float* var, const float* g, float* m, float* v, int64_t n, float alpha, float b1, float b2, float eps,
                  hipStream_t s);
 }  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Batched sampling and CartPole-v0 rollouts (rollout.hip): agent.act
+// (trpo_inksci.py:76-87), cat_sample (utils.py:95-105), rollout (utils.py:18-45)
+// ---------------------------------------------------------------------------
+struct PolicyShape {
+  int L;
+  int w[kMaxLayers + 1];
+  int64_t offW[kMaxLayers], offb[kMaxLayers];
+};
+struct RolloutArgs {
+  PolicyShape ps;
+  const float* theta;
+  int maxw;                 // max layer width (LDS slice per wave: 2 * maxw floats)
+  int n_envs, max_pathlength, time_limit, train;
+  int64_t budget;           // steps per environment: ceil(n_timesteps / n_envs)
+  int64_t env_cap;          // rows per environment region: budget + max episode length - 1
+  int max_episodes;         // second dim of reset_u
+  uint64_t seed;
+  const double* reset_u;    // optional [n_envs][max_episodes][4] uniforms for env.reset
+  const double* act_u;      // optional [n_envs][env_cap] uniforms for cat_sample
+  // per-environment regions (row = env * env_cap + i)
+  double* obs;              // [.][obs_dim]
+  int64_t* actions;
+  float* dist;              // [.][A]
+  double* rewards;
+  uint8_t* starts;
+  double* uniforms_out;     // optional: the cat_sample uniform of every step
+  int64_t* counts;          // [n_envs] steps collected
+  int64_t* episodes;        // [n_envs] episodes collected
+};
+struct RolloutOut {         // concatenated outputs; any pointer may be NULL
+  double* obs64;            // [N][obs_dim]
+  float* X;                 // [N][ldx]   (engine batch: f32 states)
+  int ldx;
+  float* dist;              // [N][A]
+  float* old;               // [N][ld_old] (engine batch: oldaction_dist)
+  int ld_old;
+  int64_t* actions64;
+  int* act32;
+  double* rewards;
+  uint8_t* starts;
+  double* uniforms;
+};
+size_t rollout_lds_bytes(int maxw);
+void launch_rollout(const RolloutArgs& a, hipStream_t s);
+void launch_rollout_compact(const RolloutArgs& a, const int64_t* offsets, const RolloutOut& o, int64_t max_count,
+                            hipStream_t s);
+void launch_act(const PolicyShape& ps, const float* theta, int maxw, const float* states, int64_t n, const double* r,
+                int train, int64_t* actions, float* dists, hipStream_t s);
+void launch_cat_sample(const float* prob, int64_t n, int k, const double* r, int64_t* out, hipStream_t s);
+void launch_cartpole_step(const double* state, const int64_t* action, int64_t n, double* state_out, double* reward,
+                          uint8_t* done, hipStream_t s);
+}  // namespace trpo

@@ -258,6 +258,81 @@ class Engine:
         check(lib.trpo_update(self._h, ctypes.byref(cp), ctypes.byref(st)), "trpo_update")
         return st.as_dict()
 
+    # ------------------------------------------------------------------ sampling / rollouts
+    def act(self, states, uniforms=None, train: bool = True):
+        """agent.act on a batch (trpo_inksci.py:76-87): (actions int64 [n], action_dist f32 [n, A])."""
+        n = int(states.shape[0])
+        s = _Arg(states, np.float32, (n, self.obs_dim))
+        if s.mem == MEM_DEVICE:
+            import torch
+            acts = torch.empty(n, dtype=torch.int64, device=s.obj.device)
+            dists = torch.empty((n, self.n_actions), dtype=torch.float32, device=s.obj.device)
+        else:
+            acts = np.empty(n, np.int64)
+            dists = np.empty((n, self.n_actions), np.float32)
+        u = _Arg(uniforms, np.float64, (n,)) if uniforms is not None else _Arg(None, np.float64)
+        a = _Arg(acts, np.int64, writable=True)
+        d = _Arg(dists, np.float32, writable=True)
+        check(lib.trpo_act(self._h, s.ptr, n, u.ptr, int(bool(train)), a.ptr, d.ptr, s.mem), "trpo_act")
+        return acts, dists
+
+    def rollout_cartpole(self, n_envs: int = 1, n_timesteps: int = 1000, max_pathlength: int = 1000,
+                         seed: int = 1, train: bool = True, time_limit: int = 200,
+                         reset_uniforms=None, action_uniforms=None, max_episodes_per_env: int = 0):
+        """rollout(env, agent, max_pathlength, n_timesteps) (utils.py:18-45) over n_envs CartPole-v0
+        instances on the GPU.  Returns (total steps, number of paths)."""
+        p = _lib.RolloutParams()
+        lib.trpo_default_rollout_params(ctypes.byref(p))
+        p.n_envs, p.n_timesteps, p.max_pathlength = int(n_envs), int(n_timesteps), int(max_pathlength)
+        p.seed, p.train, p.time_limit = int(seed) & ((1 << 64) - 1), int(bool(train)), int(time_limit)
+        keep = []
+        if reset_uniforms is not None:
+            ru = _Arg(reset_uniforms, np.float64)
+            keep.append(ru)
+            p.reset_uniforms = ru.ptr
+            p.max_episodes_per_env = int(max_episodes_per_env)
+            p.mem = ru.mem
+        if action_uniforms is not None:
+            au = _Arg(action_uniforms, np.float64)
+            keep.append(au)
+            p.action_uniforms = au.ptr
+            p.mem = au.mem
+        n = ctypes.c_int64(0)
+        paths = ctypes.c_int64(0)
+        check(lib.trpo_rollout_cartpole(self._h, ctypes.byref(p), ctypes.byref(n), ctypes.byref(paths)),
+              "trpo_rollout_cartpole")
+        self.rollout_steps = n.value
+        return n.value, paths.value
+
+    def rollout_fetch(self, device=None):
+        """The concatenated rollout as the reference's arrays: obs f64 [N,4], actions i64, action_dists
+        f32 [N,A], rewards f64, episode starts u8, cat_sample uniforms f64 (numpy, or torch on `device`)."""
+        N = self.rollout_steps
+        if device is not None:
+            import torch
+            mk = lambda shape, dt: torch.empty(shape, dtype=dt, device=device)   # noqa: E731
+            out = {"obs": mk((N, self.obs_dim), torch.float64), "actions": mk(N, torch.int64),
+                   "action_dists": mk((N, self.n_actions), torch.float32), "rewards": mk(N, torch.float64),
+                   "starts": mk(N, torch.uint8), "uniforms": mk(N, torch.float64)}
+            mem = MEM_DEVICE
+            ptr = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+        else:
+            out = {"obs": np.empty((N, self.obs_dim)), "actions": np.empty(N, np.int64),
+                   "action_dists": np.empty((N, self.n_actions), np.float32), "rewards": np.empty(N),
+                   "starts": np.empty(N, np.uint8), "uniforms": np.empty(N)}
+            mem = MEM_HOST
+            ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)   # noqa: E731
+        check(lib.trpo_rollout_fetch(self._h, ptr(out["obs"]), ptr(out["actions"]), ptr(out["action_dists"]),
+                                     ptr(out["rewards"]), ptr(out["starts"]), ptr(out["uniforms"]), mem),
+              "trpo_rollout_fetch")
+        return out
+
+    def rollout_to_batch(self, n_global: Optional[int] = None):
+        """Load the rollout as the feed (states, actions, oldaction_dist, rewards, path starts) on the device."""
+        N = self.rollout_steps
+        check(lib.trpo_rollout_to_batch(self._h, N if n_global is None else int(n_global)), "trpo_rollout_to_batch")
+        self.n, self.n_global = N, (N if n_global is None else int(n_global))
+
     # ------------------------------------------------------------------ profiling
     def profile_enable(self, on: bool = True):
         check(lib.trpo_profile_enable(self._h, int(bool(on))), "trpo_profile_enable")
@@ -272,6 +347,30 @@ class Engine:
         buf = ctypes.create_string_buffer(need + 1)
         lib.trpo_profile_query(self._h, buf, need + 1)
         return json.loads(buf.value.decode())
+
+
+def cat_sample_device(prob_nk, uniforms) -> np.ndarray:
+    """cat_sample (utils.py:95-105) on the current GPU with the uniforms given."""
+    p = np.ascontiguousarray(prob_nk, np.float32)
+    r = np.ascontiguousarray(uniforms, np.float64)
+    assert p.ndim == 2 and r.shape == (p.shape[0],)
+    out = np.empty(p.shape[0], np.int64)
+    check(lib.trpo_cat_sample(p.ctypes.data_as(ctypes.c_void_p), p.shape[0], p.shape[1],
+                              r.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), MEM_HOST),
+          "trpo_cat_sample")
+    return out
+
+
+def cartpole_step_device(state, action):
+    """One CartPole-v0 step per row on the current GPU: (state_out [n,4], reward [n], done [n] bool)."""
+    s = np.ascontiguousarray(state, np.float64).reshape(-1, 4)
+    a = np.ascontiguousarray(action, np.int64).reshape(-1)
+    n = s.shape[0]
+    so, rw, dn = np.empty((n, 4)), np.empty(n), np.empty(n, np.uint8)
+    check(lib.trpo_cartpole_step(s.ctypes.data_as(ctypes.c_void_p), a.ctypes.data_as(ctypes.c_void_p), n,
+                                 so.ctypes.data_as(ctypes.c_void_p), rw.ctypes.data_as(ctypes.c_void_p),
+                                 dn.ctypes.data_as(ctypes.c_void_p), MEM_HOST), "trpo_cartpole_step")
+    return so, rw, dn.astype(bool)
 
 
 def discount_device(x, gamma: float, episode_starts=None) -> np.ndarray:
