@@ -205,13 +205,33 @@ typedef struct trpo_rollout_params {
 void trpo_default_rollout_params(trpo_rollout_params* p);
 /* run the rollout; returns the total steps N and the number of paths */
 int trpo_rollout_cartpole(trpo_engine* e, const trpo_rollout_params* p, int64_t* n_steps_out, int64_t* n_paths_out);
-/* the concatenated paths (utils.py:36-39): obs [N][4] f64, actions [N] i64, action_dists [N][A] f32,
- * rewards [N] f64, episode_starts [N] u8, and the cat_sample uniform of every step; any may be NULL */
-int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* action_dists, double* rewards,
-                       uint8_t* episode_starts, double* uniforms, int mem);
+/* the concatenated paths (utils.py:36-39): obs [N][4] f64 (and/or as the float32 the placeholders
+ * receive), actions [N] i64, action_dists [N][A] f32, rewards [N] f64, episode_starts [N] u8, and the
+ * cat_sample uniform of every step; any may be NULL */
+int trpo_rollout_fetch(trpo_engine* e, double* obs, float* obs32, int64_t* actions, float* action_dists,
+                       double* rewards, uint8_t* episode_starts, double* uniforms, int mem);
 /* the rollout becomes the feed on the device (trpo_inksci.py:108-112,119-122): states, actions,
  * oldaction_dist, rewards and path starts, with no host round trip; baseline cleared */
 int trpo_rollout_to_batch(trpo_engine* e, int64_t n_global);
+/* Device pointers into the current feed, for other device-side consumers (the VF) to read in place;
+ * synchronises the engine stream first. */
+typedef struct trpo_feed_view {
+  int64_t n, n_global;
+  int obs_dim, n_actions;
+  const float* states;       /* [n][ld_states] f32 */
+  int ld_states;
+  const float* old_dist;     /* [n][ld_old] f32 */
+  int ld_old;
+  const uint8_t* episode_starts;   /* [n] */
+  const double* returns;     /* [n] f64, valid after the advantages were computed */
+  double* baseline;          /* [n] f64; trpo_set_baseline(e, view.baseline, TRPO_MEM_DEVICE) marks it set */
+} trpo_feed_view;
+int trpo_get_feed_view(trpo_engine* e, trpo_feed_view* out);
+/* set only the baseline [n] f64 of the current feed (VF.predict output, trpo_inksci.py:103) */
+int trpo_set_baseline(trpo_engine* e, const double* baseline, int mem);
+/* explained_variance(baseline, returns) (utils.py:208-211, trpo_inksci.py:167) over the current
+ * feed (all ranks), after the returns were computed; NaN when var(returns) == 0 */
+int trpo_explained_variance(trpo_engine* e, double* out);
 /* agent.act on n states [n][obs_dim] f32 (trpo_inksci.py:76-87): action_dist at the current
  * parameters and cat_sample against `uniforms` [n] (train = 1) or argmax (train = 0) */
 int trpo_act(trpo_engine* e, const float* states, int64_t n, const double* uniforms, int train, int64_t* actions_out,
@@ -247,6 +267,8 @@ int trpo_vf_get_optimizer(trpo_vf* vf, float* m_out, float* v_out, float powers_
  * steps from each path start.  n_global = rows over all ranks. */
 int trpo_vf_set_features(trpo_vf* vf, int64_t n, int64_t n_global, const float* obs, int obs_dim,
                          const float* action_dists, int n_actions, const uint8_t* episode_starts, int mem);
+/* ... or from an engine's feed in place (trpo_get_feed_view), targets = its returns when with_targets */
+int trpo_vf_set_features_view(trpo_vf* vf, const trpo_feed_view* view, int with_targets);
 /* ... or take a ready feature matrix [n][feat_dim] f32 */
 int trpo_vf_set_feature_matrix(trpo_vf* vf, int64_t n, int64_t n_global, const float* feat, int mem);
 int trpo_vf_get_feature_matrix(trpo_vf* vf, float* feat_out, int mem);

@@ -42,6 +42,12 @@ class RolloutParams(ctypes.Structure):
                 ("action_uniforms", c_void_p), ("max_episodes_per_env", c_int), ("mem", c_int)]
 
 
+class FeedView(ctypes.Structure):
+    _fields_ = [("n", c_int64), ("n_global", c_int64), ("obs_dim", c_int), ("n_actions", c_int),
+                ("states", c_void_p), ("ld_states", c_int), ("old_dist", c_void_p), ("ld_old", c_int),
+                ("episode_starts", c_void_p), ("returns", c_void_p), ("baseline", c_void_p)]
+
+
 FAX_CB = CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p)
 ALLREDUCE_CB = CFUNCTYPE(c_int, c_void_p, c_int64, c_int, c_void_p)
 F32, F64 = 0, 1
@@ -84,7 +90,12 @@ SIGNATURES = {
     # sampling / rollouts (trpo_inksci.py:76-87, utils.py:18-45,95-105)
     "trpo_default_rollout_params": (None, [POINTER(RolloutParams)]),
     "trpo_rollout_cartpole": (c_int, [c_void_p, POINTER(RolloutParams), POINTER(c_int64), POINTER(c_int64)]),
-    "trpo_rollout_fetch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "trpo_rollout_fetch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_int]),
+    "trpo_set_baseline": (c_int, [c_void_p, c_void_p, c_int]),
+    "trpo_get_feed_view": (c_int, [c_void_p, POINTER(FeedView)]),
+    "trpo_vf_set_features_view": (c_int, [c_void_p, POINTER(FeedView), c_int]),
+    "trpo_explained_variance": (c_int, [c_void_p, POINTER(c_double)]),
     "trpo_rollout_to_batch": (c_int, [c_void_p, c_int64]),
     "trpo_act": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int]),
     "trpo_cat_sample": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int]),

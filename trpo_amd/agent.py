@@ -10,19 +10,25 @@ Two ways to run one policy update, both on the GPU:
   ``linesearch``, ``GetFlat``/``SetFromFlat``), i.e. what
   ``trpo_inksci.py`` looks like once its TF session is replaced.
 
-Rollout and the value-function baseline are outside the hot path (SURVEY.md
-§8(f)); paths come in as the reference's dicts (``utils.py:36-39``) with an
-optional ``"baseline"`` entry (zeros otherwise, as ``VF.predict`` returns before
-its first fit, ``utils.py:88-89``).
+* :meth:`TRPOAgent.learn` — the whole loop of ``trpo_inksci.py:89-177`` on the
+  device: CartPole-v0 rollouts (``rollout.hip``), VF baselines and fit
+  (``vf.hip``), advantages, the update, explained variance and the reference's
+  stop rules; only the print-out statistics come back to the host.
+
+For the update methods, paths come in as the reference's dicts
+(``utils.py:36-39``) with an optional ``"baseline"`` entry (zeros otherwise, as
+``VF.predict`` returns before its first fit, ``utils.py:88-89``).
 """
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Sequence
+import time
+from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 
 from .engine import Engine, UpdateParams
+from .vf import VF
 from .utils import (EngineLoss, FisherVectorProduct, GetFlat, SetFromFlat, SurrogateLoss,
                     conjugate_gradient, flatgrad, linesearch)
 
@@ -33,8 +39,19 @@ CONFIG = {"max_steps": 1000, "episodes_per_roll": 1000, "gamma": 0.95, "cg_dampi
 class Session:
     """Stands in for the ``tf.Session`` the reference threads through utils (trpo_inksci.py:23)."""
 
-    def __init__(self, engine: Engine):
+    def __init__(self, engine: Engine, init_rng: Optional[np.random.RandomState] = None,
+                 reinit_policy: bool = True):
         self.engine = engine
+        self.init_rng = init_rng or np.random.RandomState(1)
+        self.reinit_policy = reinit_policy
+
+    def initialize_all_variables(self):
+        """tf.initialize_all_variables() re-draws every variable, the policy included; the reference
+        runs it again when the VF creates its net (utils.py:66), so its first update starts from a
+        fresh initialisation.  reinit_policy=False keeps the current policy instead."""
+        if self.reinit_policy:
+            e = self.engine
+            self.engine.set_flat(xavier_theta(e.obs_dim, e.hidden, e.n_actions, self.init_rng))
 
 
 def xavier_theta(obs_dim: int, hidden: Sequence[int], n_actions: int,
@@ -74,14 +91,18 @@ def paths_to_batch(paths: List[Dict]) -> Dict[str, np.ndarray]:
 
 class TRPOAgent:
     def __init__(self, obs_dim: int, n_actions: int, hidden: Sequence[int] = (64,), max_rows: int = 4096,
-                 device: int = 0, theta: Optional[np.ndarray] = None, config: Optional[dict] = None):
+                 device: int = 0, theta: Optional[np.ndarray] = None, config: Optional[dict] = None,
+                 reinit_policy: bool = True):
         self.config = dict(CONFIG if config is None else config)
         self.engine = Engine(obs_dim, hidden, n_actions, max_rows, device)
-        self.session = Session(self.engine)
+        self.session = Session(self.engine, reinit_policy=reinit_policy)
         self.gf = GetFlat(self.session)                          # trpo_inksci.py:71
         self.sff = SetFromFlat(self.session)                     # :72
         self.pg = flatgrad(SurrogateLoss(self.engine))           # :54
-        self.sff(xavier_theta(obs_dim, hidden, n_actions) if theta is None else theta)
+        self.sff(xavier_theta(obs_dim, hidden, n_actions, self.session.init_rng) if theta is None else theta)
+        self.train = True                                        # :28
+        self.end_count = 0                                       # :29
+        self.vf = VF(self.session, max_rows=max_rows, device=device)   # :73
 
     def feed(self, paths_or_batch, n_global: Optional[int] = None):
         """The feed dict of trpo_inksci.py:119-122 (+ rewards for :102-117)."""
@@ -122,3 +143,71 @@ class TRPOAgent:
             self.sff(thprev)
         return {"surr_after": float(surrafter), "kl_after": float(kloldnew), "ent_after": float(entropy),
                 "reverted": reverted, "shs": shs, "lm": float(lm)}
+
+    # ------------------------------------------------------------------ trpo_inksci.py:89-177
+    def learn(self, max_iterations: Optional[int] = None, n_envs: int = 1, seed: int = 1,
+              log: Optional[Callable[[str], None]] = print) -> List[dict]:
+        """The reference's learn() loop on CartPole-v0, device-resident.  Stop rules as
+        trpo_inksci.py:131-141,172-175: training stops when the mean episode reward exceeds
+        1.1*500 or the baseline explains > 0.8 of the returns' variance; the loop then keeps
+        rolling out the argmax policy and ends after 100 such iterations; a NaN entropy ends it
+        (the reference calls exit(-1)).  max_iterations bounds the loop (None: as the reference).
+        Returns one stats dict per iteration."""
+        cfg = self.config
+        eng = self.engine
+        say = log or (lambda _s: None)
+        start_time = time.time()
+        i = 0
+        numeptotal = 0
+        history = []
+        while max_iterations is None or i < max_iterations:
+            say("Rollout")
+            n, n_paths = eng.rollout_cartpole(n_envs=n_envs, n_timesteps=cfg["episodes_per_roll"],
+                                              max_pathlength=cfg["max_steps"], seed=seed * 1000003 + i,
+                                              train=self.train)                          # :96-100
+            eng.rollout_to_batch()                                                       # :108-122
+            self.vf.predict_engine(eng)                                                  # :103
+            eng.compute_advantages_device(cfg["gamma"])                                  # :104-117
+            ep = eng.rollout_fetch_stats()
+            episoderewards = np.add.reduceat(ep["rewards"], np.flatnonzero(ep["starts"]))   # :131
+            say("\n********** Iteration %i ************" % i)
+            rec = {"iteration": i, "steps": n, "paths": n_paths, "train": self.train,
+                   "reward_mean": float(episoderewards.mean())}
+            if episoderewards.mean() > 1.1 * 500:                                        # :135-136
+                self.train = False
+            if not self.train:                                                           # :137-141
+                say("Episode mean: %f" % episoderewards.mean())
+                self.end_count += 1
+                if self.end_count > 100:
+                    history.append(rec)
+                    break
+            if self.train:
+                self.vf.fit_engine(eng)                                                  # :143
+                st = eng.update(UpdateParams(cg_iters=10, residual_tol=1e-10, cg_damping=cfg["cg_damping"],
+                                             max_kl=cfg["max_kl"], compute_advantages=False))     # :144-158
+                numeptotal += len(episoderewards)
+                exp = eng.explained_variance()                                           # :167
+                stats = {
+                    "Total number of episodes": numeptotal,
+                    "Average sum of rewards per episode": episoderewards.mean(),
+                    "Entropy": st["ent_after"],
+                    "Baseline explained": exp,
+                    "Time elapsed": "%.2f mins" % ((time.time() - start_time) / 60.0),
+                    "KL between old and new distribution": st["kl_after"],
+                    "Surrogate loss": st["surr_after"],
+                }
+                for k, v in stats.items():
+                    say(k + ": " + " " * (40 - len(k)) + str(v))
+                rec.update({"entropy": float(st["ent_after"]), "kl": float(st["kl_after"]),
+                            "surr": float(st["surr_after"]), "explained_variance": float(exp),
+                            "reverted": bool(st["reverted"]), "k": int(st["k"]), "episodes": numeptotal})
+                history.append(rec)
+                if st["ent_after"] != st["ent_after"]:                                    # :172-173
+                    rec["nan_exit"] = True
+                    break
+                if exp > 0.8:                                                            # :174-175
+                    self.train = False
+            else:
+                history.append(rec)
+            i += 1
+        return history

@@ -69,7 +69,8 @@ struct trpo_engine {
   float *adv32 = nullptr, *old = nullptr;
   double *rewards = nullptr, *returns = nullptr, *adv64 = nullptr, *baseline = nullptr;
   uint8_t* starts = nullptr;
-  bool have_baseline = false, have_rewards = false;
+  bool have_baseline = false, have_rewards = false, have_returns = false;
+  double* ev_tmp = nullptr;   // explained_variance scratch
   std::vector<float*> H, D, E, RH, RD;   // indexed as in DESIGN.md
   float *Pm = nullptr, *DSL = nullptr;
   double* rowterms = nullptr;
@@ -956,6 +957,29 @@ struct trpo_engine {
     launch_adv_normalize(adv64, adv32, n, dscal, dscal + 1, inv_n, stream);
     check_launch();
     prepared = false;
+    have_returns = true;
+  }
+
+  // 1 - var(y - ypred)/var(y) with y = returns, ypred = baseline (utils.py:208-211), f64 over all ranks
+  double explained_variance() {
+    REQUIRE(have_returns, "no returns: compute the advantages first");
+    if (!ev_tmp) ev_tmp = dalloc<double>(cap);
+    const double inv_n = 1.0 / (double)n_global;
+    auto var = [&](const double* ypred, int slot) {
+      launch_adv_center_partials(returns, ypred, ev_tmp, n, partA, stream);
+      launch_sum_finish(partA, dscal + slot, stream);
+      allreduce_f64(dscal + slot, 1);
+      launch_adv_sq_partials(ev_tmp, n, dscal + slot, inv_n, partA, stream);
+      launch_sum_finish(partA, dscal + slot + 1, stream);
+      allreduce_f64(dscal + slot + 1, 1);
+      check_launch();
+    };
+    var(nullptr, 2);
+    var(have_baseline ? baseline : nullptr, 4);
+    double h[6];
+    copy_out(h, dscal, sizeof h, TRPO_MEM_HOST);
+    const double vary = h[3] * inv_n, vard = h[5] * inv_n;
+    return vary == 0.0 ? std::nan("") : 1.0 - vard / vary;
   }
 
   void update(const trpo_update_params& prm, trpo_update_stats* st) {
@@ -1177,6 +1201,7 @@ int trpo_set_batch(trpo_engine* e, int64_t n, int64_t n_global, const float* sta
     e->set_splits();
     e->prepared = false;
     e->have_rewards = false;
+    e->have_returns = false;
   });
 }
 
@@ -1191,6 +1216,7 @@ int trpo_set_rewards(trpo_engine* e, const double* rewards, const uint8_t* start
     e->have_baseline = baseline != nullptr;
     if (baseline) e->copy_in(e->baseline, baseline, (size_t)e->n * sizeof(double), mem);
     e->have_rewards = true;
+    e->have_returns = false;
   });
 }
 
@@ -1441,8 +1467,8 @@ int trpo_rollout_cartpole(trpo_engine* e, const trpo_rollout_params* p, int64_t*
   });
 }
 
-int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* action_dists, double* rewards,
-                       uint8_t* episode_starts, double* uniforms, int mem) {
+int trpo_rollout_fetch(trpo_engine* e, double* obs, float* obs32, int64_t* actions, float* action_dists,
+                       double* rewards, uint8_t* episode_starts, double* uniforms, int mem) {
   return guarded([&] {
     REQUIRE(e, "NULL argument");
     REQUIRE(e->roll_valid, "no rollout to fetch");
@@ -1460,6 +1486,8 @@ int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* act
       return static_cast<T*>(ptr);
     };
     o.obs64 = dst(obs, (size_t)N * obs_dim);
+    o.X = dst(obs32, (size_t)N * obs_dim);
+    o.ldx = obs_dim;
     o.actions64 = dst(actions, (size_t)N);
     o.dist = dst(action_dists, (size_t)N * A);
     o.rewards = dst(rewards, (size_t)N);
@@ -1469,6 +1497,7 @@ int trpo_rollout_fetch(trpo_engine* e, double* obs, int64_t* actions, float* act
       e->rollout_compact(o);
       if (mem != TRPO_MEM_DEVICE) {
         if (obs) e->copy_out(obs, o.obs64, (size_t)N * obs_dim * sizeof(double), mem);
+        if (obs32) e->copy_out(obs32, o.X, (size_t)N * obs_dim * sizeof(float), mem);
         if (actions) e->copy_out(actions, o.actions64, (size_t)N * sizeof(int64_t), mem);
         if (action_dists) e->copy_out(action_dists, o.dist, (size_t)N * A * sizeof(float), mem);
         if (rewards) e->copy_out(rewards, o.rewards, (size_t)N * sizeof(double), mem);
@@ -1506,8 +1535,47 @@ int trpo_rollout_to_batch(trpo_engine* e, int64_t n_global) {
     e->set_splits();
     e->prepared = false;
     e->have_rewards = true;
+    e->have_returns = false;
     e->have_baseline = false;
     HIPCHECK(hipStreamSynchronize(e->stream));
+  });
+}
+
+int trpo_get_feed_view(trpo_engine* e, trpo_feed_view* v) {
+  return guarded([&] {
+    REQUIRE(e && v, "NULL argument");
+    e->require_batch();
+    e->use();
+    HIPCHECK(hipStreamSynchronize(e->stream));   // other streams read these buffers next
+    v->n = e->n;
+    v->n_global = e->n_global;
+    v->obs_dim = e->w[0];
+    v->n_actions = e->w[e->L];
+    v->states = e->X;
+    v->ld_states = e->wp[0];
+    v->old_dist = e->old;
+    v->ld_old = e->wp[e->L];
+    v->episode_starts = e->have_rewards ? e->starts : nullptr;
+    v->returns = e->returns;
+    v->baseline = e->baseline;
+  });
+}
+
+int trpo_set_baseline(trpo_engine* e, const double* baseline, int mem) {
+  return guarded([&] {
+    REQUIRE(e && baseline, "NULL argument");
+    e->require_batch();
+    e->use();
+    if (baseline != e->baseline) e->copy_in(e->baseline, baseline, (size_t)e->n * sizeof(double), mem);
+    e->have_baseline = true;
+  });
+}
+
+int trpo_explained_variance(trpo_engine* e, double* out) {
+  return guarded([&] {
+    REQUIRE(e && out, "NULL argument");
+    e->use();
+    *out = e->explained_variance();
   });
 }
 

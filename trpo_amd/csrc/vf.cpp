@@ -388,6 +388,26 @@ int trpo_vf_set_features(trpo_vf* e, int64_t n, int64_t n_global, const float* o
   });
 }
 
+int trpo_vf_set_features_view(trpo_vf* e, const trpo_feed_view* v, int with_targets) {
+  return guarded([&] {
+    REQUIRE(e && v && v->states && v->old_dist, "NULL argument");
+    REQUIRE(v->obs_dim + v->n_actions + 1 == e->F, "feat_dim must equal obs_dim + n_actions + 1 (utils.py:70-77)");
+    e->use();
+    e->set_rows(v->n, v->n_global);
+    launch_vf_features(v->states, v->obs_dim, v->ld_states, v->old_dist, v->n_actions, v->ld_old, v->episode_starts,
+                       v->n, e->lastpos, e->pos_ws, e->feat, e->Fp, e->stream);
+    check_launch();
+    if (with_targets) {
+      REQUIRE(v->returns, "view has no returns");
+      launch_f64_to_f32(v->returns, e->tgt, e->n, e->stream);
+      check_launch();
+    }
+    HIPCHECK(hipStreamSynchronize(e->stream));
+    e->have_feat = true;
+    if (with_targets) e->have_tgt = true;
+  });
+}
+
 int trpo_vf_set_feature_matrix(trpo_vf* e, int64_t n, int64_t n_global, const float* feat, int mem) {
   return guarded([&] {
     REQUIRE(e && feat, "NULL argument");

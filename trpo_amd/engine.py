@@ -187,6 +187,35 @@ class Engine:
         b = _Arg(baseline, np.float64, (n,)) if baseline is not None else _Arg(None, np.float64)
         check(lib.trpo_set_rewards(self._h, r.ptr, st.ptr, b.ptr, r.mem), "trpo_set_rewards")
 
+    def set_baseline(self, baseline):
+        """The VF.predict baselines of the current feed (trpo_inksci.py:103), f64 [n]."""
+        b = _Arg(baseline, np.float64, (self.n,))
+        check(lib.trpo_set_baseline(self._h, b.ptr, b.mem), "trpo_set_baseline")
+
+    def feed_view(self) -> "_lib.FeedView":
+        """Device pointers into the current feed (synchronises the engine stream)."""
+        v = _lib.FeedView()
+        check(lib.trpo_get_feed_view(self._h, ctypes.byref(v)), "trpo_get_feed_view")
+        return v
+
+    def set_baseline_in_place(self):
+        """Mark the feed's own baseline buffer (written through feed_view().baseline) as set."""
+        v = self.feed_view()
+        check(lib.trpo_set_baseline(self._h, v.baseline, MEM_DEVICE), "trpo_set_baseline")
+
+    def explained_variance(self) -> float:
+        """explained_variance(baseline, returns) (utils.py:208-211) over the feed, on the device."""
+        out = ctypes.c_double(0.0)
+        check(lib.trpo_explained_variance(self._h, ctypes.byref(out)), "trpo_explained_variance")
+        return out.value
+
+    def compute_advantages_device(self, gamma: float, returns_out=None, advant_out=None):
+        """trpo_inksci.py:102-117 on the device; optional device/host outputs (f64 [n])."""
+        r = _Arg(returns_out, np.float64, (self.n,), writable=True) if returns_out is not None else _Arg(None, np.float64)
+        a = _Arg(advant_out, np.float64, (self.n,), writable=True) if advant_out is not None else _Arg(None, np.float64)
+        mem = r.mem if r.ptr is not None else (a.mem if a.ptr is not None else MEM_HOST)
+        check(lib.trpo_compute_advantages(self._h, float(gamma), r.ptr, a.ptr, mem), "trpo_compute_advantages")
+
     def compute_advantages(self, gamma: float = 0.95):
         ret = np.empty(self.n, np.float64)
         adv = np.empty(self.n, np.float64)
@@ -305,27 +334,40 @@ class Engine:
         return n.value, paths.value
 
     def rollout_fetch(self, device=None):
-        """The concatenated rollout as the reference's arrays: obs f64 [N,4], actions i64, action_dists
-        f32 [N,A], rewards f64, episode starts u8, cat_sample uniforms f64 (numpy, or torch on `device`)."""
+        """The concatenated rollout as the reference's arrays: obs f64 [N,4] (and f32), actions i64,
+        action_dists f32 [N,A], rewards f64, episode starts u8, cat_sample uniforms f64 (numpy, or torch
+        tensors on `device` -- torch must have initialised its GPU context before the first engine was
+        created: it bundles its own HIP runtime, which cannot start after ours)."""
         N = self.rollout_steps
         if device is not None:
             import torch
             mk = lambda shape, dt: torch.empty(shape, dtype=dt, device=device)   # noqa: E731
-            out = {"obs": mk((N, self.obs_dim), torch.float64), "actions": mk(N, torch.int64),
+            out = {"obs": mk((N, self.obs_dim), torch.float64), "obs32": mk((N, self.obs_dim), torch.float32),
+                   "actions": mk(N, torch.int64),
                    "action_dists": mk((N, self.n_actions), torch.float32), "rewards": mk(N, torch.float64),
                    "starts": mk(N, torch.uint8), "uniforms": mk(N, torch.float64)}
             mem = MEM_DEVICE
             ptr = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
         else:
-            out = {"obs": np.empty((N, self.obs_dim)), "actions": np.empty(N, np.int64),
+            out = {"obs": np.empty((N, self.obs_dim)), "obs32": np.empty((N, self.obs_dim), np.float32),
+                   "actions": np.empty(N, np.int64),
                    "action_dists": np.empty((N, self.n_actions), np.float32), "rewards": np.empty(N),
                    "starts": np.empty(N, np.uint8), "uniforms": np.empty(N)}
             mem = MEM_HOST
             ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)   # noqa: E731
-        check(lib.trpo_rollout_fetch(self._h, ptr(out["obs"]), ptr(out["actions"]), ptr(out["action_dists"]),
+        check(lib.trpo_rollout_fetch(self._h, ptr(out["obs"]), ptr(out["obs32"]), ptr(out["actions"]),
+                                     ptr(out["action_dists"]),
                                      ptr(out["rewards"]), ptr(out["starts"]), ptr(out["uniforms"]), mem),
               "trpo_rollout_fetch")
         return out
+
+    def rollout_fetch_stats(self):
+        """Rewards and path starts of the last rollout (host; for the print-out statistics)."""
+        N = self.rollout_steps
+        rew, st = np.empty(N), np.empty(N, np.uint8)
+        check(lib.trpo_rollout_fetch(self._h, None, None, None, None, rew.ctypes.data_as(ctypes.c_void_p),
+                                     st.ctypes.data_as(ctypes.c_void_p), None, MEM_HOST), "trpo_rollout_fetch")
+        return {"rewards": rew, "starts": st}
 
     def rollout_to_batch(self, n_global: Optional[int] = None):
         """Load the rollout as the feed (states, actions, oldaction_dist, rewards, path starts) on the device."""

@@ -16,6 +16,12 @@ conjugate_gradient :185-201   ``conjugate_gradient(f_Ax, b, ...)``       device 
                                                                           device-resident)
 var_shape/numel :108-116      same                                       shapes only
 explained_variance :208-211   same                                       numpy (statistics print-out)
+rollout         :18-45        ``rollout(env, agent, max_pathlength, n)`` host loop over any env; the
+                                                                          CartPole-v0 batch runs on the
+                                                                          device (``Engine.rollout_cartpole``)
+VF              :48-92        ``VF(session)``                            device MLP fit / predict (vf.hip)
+cat_sample      :95-105       ``cat_sample(prob_nk)``                    device inverse-CDF sampling
+dict2           :203-206      same                                       -
 ============================  =========================================  ===============================
 
 ``session`` here is a :class:`trpo_amd.agent.Session` (or anything with an
@@ -25,10 +31,12 @@ from __future__ import annotations
 
 import numpy as np
 
-from .engine import Engine, cg_callback, discount_device
+from .engine import Engine, cat_sample_device, cg_callback, discount_device
+from .vf import VF  # noqa: F401  (utils.py:48-92)
 
 __all__ = ["discount", "conjugate_gradient", "linesearch", "flatgrad", "GetFlat", "SetFromFlat",
-           "var_shape", "numel", "explained_variance", "FisherVectorProduct", "SurrogateLoss"]
+           "var_shape", "numel", "explained_variance", "FisherVectorProduct", "SurrogateLoss", "VF",
+           "cat_sample", "rollout", "dict2"]
 
 
 def _engine_of(session) -> Engine:
@@ -178,3 +186,47 @@ def explained_variance(ypred, y):
     assert y.ndim == 1 and ypred.ndim == 1
     vary = np.var(y)
     return np.nan if vary == 0 else 1 - np.var(y - ypred) / vary
+
+
+# ---------------------------------------------------------------------------- utils.py:18-45
+def rollout(env, agent, max_pathlength, n_timesteps):
+    """utils.py:18-45 for any gym-style env and an agent with act()/prev_action: whole episodes until
+    n_timesteps steps are collected.  (For CartPole-v0 the batched device rollout
+    ``Engine.rollout_cartpole`` does this for many environments at once.)  A path is kept when its
+    episode ends (done) or reaches max_pathlength."""
+    paths = []
+    steps = 0
+    while steps < n_timesteps:
+        obs, actions, rewards, action_dists = [], [], [], []
+        ob = env.reset()
+        agent.prev_action *= 0.0
+        for _ in range(max_pathlength):
+            action, action_dist, ob_in = agent.act(ob)
+            obs.append(ob_in)
+            actions.append(action)
+            action_dists.append(action_dist)
+            ob, reward, done = env.step(action)[:3]
+            rewards.append(reward)
+            if done:
+                agent.prev_action *= 0.0
+                break
+        paths.append({"obs": np.concatenate(np.expand_dims(obs, 0)), "action_dists": np.concatenate(action_dists),
+                      "rewards": np.array(rewards), "actions": np.array(actions)})
+        steps += len(rewards)
+    return paths
+
+
+# ---------------------------------------------------------------------------- utils.py:95-105
+def cat_sample(prob_nk):
+    """Inverse-CDF sampling of each row of prob_nk against np.random.rand(N), on the GPU."""
+    prob_nk = np.asarray(prob_nk)
+    assert prob_nk.ndim == 2
+    r = np.random.rand(prob_nk.shape[0])
+    return cat_sample_device(prob_nk.astype(np.float32), r).astype("i")
+
+
+# ---------------------------------------------------------------------------- utils.py:203-206
+class dict2(dict):
+    def __init__(self, **kwargs):
+        dict.__init__(self, kwargs)
+        self.__dict__ = self

@@ -132,6 +132,17 @@ class VFNet:
                                        A, s.ptr, o.mem), "trpo_vf_set_features")
         self.n = n
 
+    def set_features_view(self, view, with_targets: bool = False):
+        """Features (and the returns as targets) read in place from an engine feed view."""
+        check(lib.trpo_vf_set_features_view(self._h, ctypes.byref(view), int(bool(with_targets))),
+              "trpo_vf_set_features_view")
+        self.n = int(view.n)
+
+    def predict_to_device(self, ptr: int, dtype=np.float64):
+        """predict into a device buffer (raw pointer) of this GPU."""
+        check(lib.trpo_vf_predict(self._h, ctypes.c_void_p(ptr), _lib.F64 if dtype == np.float64 else _lib.F32,
+                                  MEM_DEVICE), "trpo_vf_predict")
+
     def set_feature_matrix(self, feat, n_global: Optional[int] = None):
         n = int(feat.shape[0])
         f = _Arg(feat, np.float32, (n, self.feat_dim))
@@ -232,7 +243,27 @@ class VF(object):
         ret = self.net.predict()
         return np.reshape(ret, (ret.shape[0], ))
 
-    # ---- device-resident forms for a concatenated batch (the fused learn() loop) ----
+    # ---- device-resident forms over an engine's feed (the learn() loop) ----
+    def predict_engine(self, engine) -> bool:
+        """VF.predict for every path of the engine's feed, written into its baseline in place.
+        Before the first fit the reference predicts zeros; the feed then has no baseline."""
+        if self.net is None:
+            return False
+        view = engine.feed_view()
+        self.net.set_features_view(view)
+        self.net.predict_to_device(view.baseline)
+        engine.set_baseline_in_place()
+        return True
+
+    def fit_engine(self, engine):
+        """VF.fit on the engine's feed: features and returns read in place (advantages computed)."""
+        view = engine.feed_view()
+        if self.net is None:
+            self.create_net(int(view.obs_dim) + int(view.n_actions) + 1)
+        self.net.set_features_view(view, with_targets=True)
+        self.net.fit(FIT_STEPS)
+
+    # ---- device-resident forms for a concatenated batch ----
     def fit_batch(self, obs, action_dists, episode_starts, returns, n_global: Optional[int] = None):
         if self.net is None:
             self.create_net(int(np.prod(obs.shape[1:])) + int(action_dists.shape[-1]) + 1)
