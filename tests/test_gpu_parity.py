@@ -279,6 +279,9 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_mfma": 4}, {"chain": 0, "split_mfma": 5}, {"chain": 0, "split_mfma": 6}, {"split_mfma": 7},
     {"split_wg": 0}, {"split_wg": 1}, {"split_wg": 2}, {"split_wg": 3},
     {"split_mfma": 5, "split_wg": 1},
+    {"split_mfma": 8}, {"split_mfma": 9},                     # 128 x 256, two blocks per CU
+    {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
+    {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -286,7 +289,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain")}
+                                           "split_wg", "chain", "split_f16")}
     try:
         for k, v in opts.items():
             set_option(k, v)

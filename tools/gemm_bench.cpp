@@ -34,12 +34,17 @@ int main(int argc, char** argv) {
   float *out = dalloc((size_t)M * N), *E = dalloc((size_t)M * N, 13), *RH2 = dalloc((size_t)M * N, 14);
   float *W = dalloc(2 * K * N, 15, 0.0625f), *bias = dalloc(N);
   uint16_t* W3; CK(hipMalloc(&W3, (size_t)2 * 3 * N * K * 2));
-  SplitArgs sa{};
-  sa.n = 2;
-  sa.job[0] = SplitJob{W, W3, K, N, N, K};
-  sa.job[1] = SplitJob{W + K * N, W3 + (size_t)3 * N * K, K, N, N, K};
-  launch_split_b(sa, nullptr, 0);
-  CK(hipDeviceSynchronize());
+  auto split = [&](int f16) {
+    SplitArgs sa{};
+    sa.n = 2;
+    sa.f16 = f16;
+    sa.job[0] = SplitJob{W, W3, K, N, N, K};
+    sa.job[1] = SplitJob{W + K * N, W3 + (size_t)3 * N * K, K, N, N, K};
+    launch_split_b(sa, nullptr, 0);
+    CK(hipDeviceSynchronize());
+  };
+  int f16 = 0;
+  split(0);
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   auto mkargs = [&](RowEpi epi, int nseg, const float* Haux) {
     RowGemmArgs g{};
@@ -47,6 +52,7 @@ int main(int argc, char** argv) {
     g.seg[0] = GemmSeg{RH, W, K, N, K, W3, K, N * K};
     g.seg[1] = GemmSeg{H, W + K * N, K, N, K, W3 + (size_t)3 * N * K, K, N * K};
     g.epi = epi;
+    g.f16 = f16;
     g.ea.bias = bias; g.ea.H = Haux; g.ea.E = E; g.ea.RH = RH2; g.ea.out0 = out; g.ea.out1 = E; g.ea.ldo = N;
     return g;
   };
@@ -58,7 +64,8 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= reps;
     const double fl = 2.0 * M * N * K * nseg;
-    printf("split=%d %-24s M=%-9ld %8.3f ms  %6.1f TF/s\n", g_options.split_mfma, name, M, ms, fl / ms / 1e9);
+    printf("split=%d f16=%d %-24s M=%-9ld %8.3f ms  %6.1f TF/s\n", g_options.split_mfma, f16, name, M, ms,
+           fl / ms / 1e9);
   };
   // accuracy: out = acc (PgBwd with H = 0), sampled rows vs an fp64 host product
   auto accuracy = [&]() {
@@ -87,13 +94,18 @@ int main(int argc, char** argv) {
           refsq += s * s;
         }
     }
-    printf("split=%d accuracy: max |err|/sum|a b| = %.3e   rel-l2 = %.3e\n", g_options.split_mfma, maxrel,
+    printf("split=%d f16=%d accuracy: max |err|/sum|a b| = %.3e   rel-l2 = %.3e\n", g_options.split_mfma, f16, maxrel,
            sqrt(sumsq / refsq));
   };
-  std::vector<int> modes = {0, 5};
+  // modes: split tile config (0 = f32 MFMA), +100 = f16 planes
+  std::vector<int> modes = {0, 5, 105, 106, 102, 107, 108, 109};
   if (argc > 3) modes = {atoi(argv[3])};   // one split mode only (profiling)
   for (int mode : modes) {
-    g_options.split_mfma = mode;
+    g_options.split_mfma = mode % 100;
+    if (f16 != mode / 100) {
+      f16 = mode / 100;
+      split(f16);
+    }
     accuracy();
     run("rfwd (2seg, RHidden)", RowEpi::kRHidden, 2);
     run("rbwd (2seg, RBwd)", RowEpi::kRBwd, 2);
@@ -112,8 +124,9 @@ int main(int argc, char** argv) {
     w.seg[0] = WSeg{RH, RH2, K, N}; w.seg[1] = WSeg{H, E, K, N}; w.colsum_seg = 1;
     w.splits = (int)((M + rps - 1) / rps); w.rows_per_split = (int)rps; w.slab = slab;
     w.slab_stride = N * K + N; w.off_w = 0; w.off_b = N * K;
-    for (int mode : {0, 1, 2, 3}) {
-      g_options.split_wg = mode;
+    for (int mode : {0, 1, 2, 3, 101, 102, 103}) {
+      g_options.split_wg = mode % 100;
+      w.f16 = mode / 100;
       launch_wgrad(w, 0); CK(hipDeviceSynchronize());
       CK(hipEventRecord(a));
       for (int i = 0; i < reps; ++i) launch_wgrad(w, 0);

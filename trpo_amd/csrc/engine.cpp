@@ -85,6 +85,25 @@ struct trpo_engine {
   UpdScalars* hsc = nullptr;   // pinned host mirror
 
   bool prepared = false;
+  // f16 split GEMMs: running max |operand| slots (float bits) that set the power-of-two scales,
+  // grouped by kind, kMaxLayers slots per group (see am_*)
+  bool f16 = false;
+  unsigned* amax = nullptr;
+  unsigned* am(int group, int l) const {
+    return f16 ? amax + (size_t)(1 + group * kMaxLayers + l) * kAmaxSlot : nullptr;
+  }
+  unsigned* am_x() const { return f16 ? amax : nullptr; }
+  unsigned* am_w(int l) const { return am(0, l); }
+  unsigned* am_v(int l) const { return am(1, l); }
+  unsigned* am_wt(int l) const { return am(2, l); }
+  unsigned* am_d(int l) const { return am(3, l); }
+  unsigned* am_ds(int l) const { return am(4, l); }
+  unsigned* am_rh(int l) const { return am(5, l); }
+  unsigned* am_rd(int l) const { return am(6, l); }
+  void am_reset(unsigned* first, int count) {
+    if (first && count > 0)
+      HIPCHECK(hipMemsetAsync(first, 0, (size_t)count * kAmaxSlot * sizeof(unsigned), stream));
+  }
   bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
   bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
@@ -228,7 +247,6 @@ struct trpo_engine {
       WFt3.push_back(dalloc<uint16_t>(plane3_f(l) * 3));
     }
     X = dalloc<float>((size_t)cap * wp[0]);
-    stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     act = dalloc<int>(cap);
     adv32 = dalloc<float>(cap);
     old = dalloc<float>((size_t)cap * wp[L]);
@@ -274,6 +292,10 @@ struct trpo_engine {
     fused_head = L >= 2 && wp[L - 1] <= 256 && wp[L - 1] % 16 == 0 && wp[L] <= 32 &&
                  g_options.fused_head != 0;   // opt-in: slower than the split kernels at C4 (1 block/CU)
     head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
+    f16 = g_options.split_f16 != 0;
+    amax = dalloc<unsigned>((size_t)(1 + 7 * kMaxLayers) * kAmaxSlot);
+    // allocated last: the big activation buffers keep the placement the kernels were tuned on
+    stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
     setup_chain();
@@ -511,10 +533,12 @@ struct trpo_engine {
   }
 
   // ------------------------------------------------------------------------
-  PackArgs pack_args(const std::vector<float*>& wf, const std::vector<float*>* wb) {
+  PackArgs pack_args(const std::vector<float*>& wf, const std::vector<float*>* wb, int am_group = -1) {
     PackArgs pa{};
     pa.nl = L;
+    if (am_group >= 0) am_reset(am(am_group, 0), L);
     for (int l = 0; l < L; ++l) {
+      pa.L[l].amax = am_group >= 0 ? am(am_group, l) : nullptr;
       pa.L[l].off_w = offW[l];
       pa.L[l].a = w[l];
       pa.L[l].b = w[l + 1];
@@ -532,11 +556,11 @@ struct trpo_engine {
   size_t plane3_b(int l) const { return (size_t)wp[l] * r16(wp[l + 1]); }   // WB part: K = wp[l+1], N = wp[l]
   SplitJob job_f(const std::vector<float*>& wf, const std::vector<uint16_t*>& wf3, int l, int part) const {
     return SplitJob{wf[l] + (size_t)part * wp[l] * wp[l + 1], wf3[l] + part * 3 * plane3_f(l), wp[l], wp[l + 1],
-                    wp[l + 1], r16(wp[l])};
+                    wp[l + 1], r16(wp[l]), part ? am_v(l) : (&wf == &WFt ? am_wt(l) : am_w(l))};
   }
   SplitJob job_b(int l, int part) const {
     return SplitJob{WB[l] + (size_t)part * wp[l + 1] * wp[l], WB3[l] + part * 3 * plane3_b(l), wp[l + 1], wp[l],
-                    wp[l], r16(wp[l + 1])};
+                    wp[l], r16(wp[l + 1]), part ? am_v(l) : am_w(l)};
   }
   // attach the planes of a packed matrix part to a row-GEMM segment
   static void seg3(GemmSeg& sg, uint16_t* base, size_t plane, int part, int K) {
@@ -550,6 +574,7 @@ struct trpo_engine {
                    const std::vector<uint16_t*>& wf3, const int* skip, const char* tag) {
     if (!split_on()) return;
     SplitArgs sa{};
+    sa.f16 = f16;
     for (int l = 0; l < L; ++l) {
       const bool f = rowgemm_uses_split(wp[l + 1], RowEpi::kTanh);   // layer l's forward output
       const bool b = l >= 1 && rowgemm_uses_split(wp[l], RowEpi::kRBwd);   // backward into layer l's input
@@ -574,6 +599,7 @@ struct trpo_engine {
 
   RowGemmArgs row_args(int l_out_width, int l_out_pad) {
     RowGemmArgs a{};
+    a.f16 = f16;
     a.M = (int)n;
     a.N = l_out_width;
     a.Npad = l_out_pad;
@@ -589,6 +615,8 @@ struct trpo_engine {
       a.nseg = 1;
       a.seg[0] = GemmSeg{l == 0 ? X : hout[l], wf[l], wp[l], wp[l + 1], wp[l]};
       seg3(a.seg[0], wf3[l], plane3_f(l), 0, wp[l]);
+      a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
+      a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
       a.ea.bias = th + offb[l];
       a.ea.ldo = wp[l + 1];
       if (l < L - 1) {
@@ -604,6 +632,10 @@ struct trpo_engine {
         a.ea.adv = adv32;
         a.ea.rowterms = rowterms;
         a.ea.invN = 1.0 / (double)n_global;
+        if (head == RowEpi::kPrepHead) {
+          a.ea.amax1 = am_d(L - 1);
+          a.ea.amax2 = am_ds(L - 1);
+        }
       }
       char t[32];
       std::snprintf(t, sizeof t, "%s_l%d", tag, l);
@@ -624,15 +656,24 @@ struct trpo_engine {
 
   void require_batch() { REQUIRE(n > 0, "no batch: call trpo_set_batch first"); }
 
+  void update_x_amax() {
+    if (!f16) return;
+    am_reset(am_x(), 1);
+    launch_amax(X, n, w[0], wp[0], am_x(), stream);
+    check_launch();
+  }
+
   // policy forward + KL_ff plain backward at theta (cached over CG)
   void prepare() {
     require_batch();
     if (prepared) return;
-    PackArgs pa = pack_args(WF, &WB);
+    PackArgs pa = pack_args(WF, &WB, 0);
     launch_pack(pa, theta, 0, nullptr, stream);
     w3_valid = false;
     chain_w_valid = false;
     ensure_w3();
+    am_reset(am_d(0), L);
+    am_reset(am_ds(L - 1), 1);
     forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
     // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H
     for (int l = L - 1; l >= 1; --l) {
@@ -640,9 +681,12 @@ struct trpo_engine {
       a.nseg = 1;
       a.seg[0] = GemmSeg{D[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
       seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
+      a.seg[0].amaxA = am_d(l);
+      a.seg[0].amaxB = am_w(l);
       a.epi = RowEpi::kPrepBwd;
       a.ea.H = H[l];
       a.ea.out0 = D[l - 1];
+      a.ea.amax0 = am_d(l - 1);
       a.ea.out1 = E[l - 1];
       a.ea.ldo = wp[l];
       char t[32];
@@ -683,6 +727,7 @@ struct trpo_engine {
     a.off_w = offW[l];
     a.off_b = offb[l];
     a.skip = skip;
+    a.f16 = f16;
     Scope sp(this, tag);
     launch_wgrad(a, stream);
     check_launch();
@@ -696,14 +741,18 @@ struct trpo_engine {
     std::vector<float*> DS(L);
     DS[L - 1] = DSL;
     for (int l = 0; l < L - 1; ++l) DS[l] = RD[l];
+    am_reset(am_ds(0), L - 1);
     for (int l = L - 1; l >= 1; --l) {
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{DS[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
       seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
+      a.seg[0].amaxA = am_ds(l);
+      a.seg[0].amaxB = am_w(l);
       a.epi = RowEpi::kPgBwd;
       a.ea.H = H[l];
       a.ea.out0 = DS[l - 1];
+      a.ea.amax0 = am_ds(l - 1);
       a.ea.ldo = wp[l];
       char t[32];
       std::snprintf(t, sizeof t, "pg_bwd_l%d", l);
@@ -714,7 +763,8 @@ struct trpo_engine {
     for (int l = 0; l < L; ++l) {
       char t[32];
       std::snprintf(t, sizeof t, "pg_wgrad_l%d", l);
-      wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1]}, WSeg{}, 0, nullptr, t);
+      wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1], l == 0 ? am_x() : nullptr, am_ds(l)}, WSeg{}, 0,
+                  nullptr, t);
     }
     reduce_grad(g, nullptr);
   }
@@ -727,12 +777,14 @@ struct trpo_engine {
       return;
     }
     {
-      PackArgs pa = pack_args(WF, &WB);
+      PackArgs pa = pack_args(WF, &WB, 1);
       launch_pack(pa, v, 1, skip, stream);
       check_launch();
     }
     ensure_w3();
     split_parts(false, true, false, true, WF, WF3, skip, "split_v");
+    am_reset(am_rh(0), L);
+    am_reset(am_rd(0), L);
     // R-forward
     const int Lf = fused_head ? L - 1 : L;
     for (int l = 0; l < Lf; ++l) {
@@ -742,12 +794,17 @@ struct trpo_engine {
         a.nseg = 1;
         a.seg[0] = GemmSeg{X, Vpart, wp[0], wp[1], wp[0]};
         seg3(a.seg[0], WF3[l], plane3_f(l), 1, wp[l]);
+        a.seg[0].amaxA = am_x();
+        a.seg[0].amaxB = am_v(0);
       } else {
         a.nseg = 2;
         a.seg[0] = GemmSeg{RH[l], WF[l], wp[l], wp[l + 1], wp[l]};
         a.seg[1] = GemmSeg{H[l], Vpart, wp[l], wp[l + 1], wp[l]};
         seg3(a.seg[0], WF3[l], plane3_f(l), 0, wp[l]);
         seg3(a.seg[1], WF3[l], plane3_f(l), 1, wp[l]);
+        a.seg[0].amaxA = am_rh(l);
+        a.seg[0].amaxB = am_w(l);
+        a.seg[1].amaxB = am_v(l);
       }
       a.skip = skip;
       a.ea.bias = v + offb[l];
@@ -756,10 +813,12 @@ struct trpo_engine {
         a.epi = RowEpi::kRHidden;
         a.ea.H = H[l + 1];
         a.ea.out0 = RH[l + 1];
+        a.ea.amax0 = am_rh(l + 1);
       } else {
         a.epi = RowEpi::kRHead;
         a.ea.P = Pm;
         a.ea.out0 = RD[L - 1];
+        a.ea.amax0 = am_rd(L - 1);
         a.ea.invN = 1.0 / (double)n_global;
       }
       char tag[32];
@@ -798,6 +857,7 @@ struct trpo_engine {
       Scope sp(this, tag);
       launch_fvp_head(h, stream);
       check_launch();
+      if (f16) launch_amax(RD[l - 1], n, w[l], wp[l], am_rd(l - 1), stream);
     }
     if (head_bwd) {
       HeadBwdArgs h{};
@@ -826,6 +886,7 @@ struct trpo_engine {
       Scope sp(this, tag);
       launch_head_bwd(h, stream);
       check_launch();
+      if (f16) launch_amax(RD[l - 1], n, w[l], wp[l], am_rd(l - 1), stream);
     }
     const bool tail_fused = fused_head || head_bwd;
     // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
@@ -836,12 +897,17 @@ struct trpo_engine {
       a.seg[1] = GemmSeg{D[l], WB[l] + (size_t)wp[l + 1] * wp[l], wp[l + 1], wp[l], wp[l + 1]};
       seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
       seg3(a.seg[1], WB3[l], plane3_b(l), 1, wp[l + 1]);
+      a.seg[0].amaxA = am_rd(l);
+      a.seg[0].amaxB = am_w(l);
+      a.seg[1].amaxA = am_d(l);
+      a.seg[1].amaxB = am_v(l);
       a.skip = skip;
       a.epi = RowEpi::kRBwd;
       a.ea.H = H[l];
       a.ea.E = E[l - 1];
       a.ea.RH = RH[l];
       a.ea.out0 = RD[l - 1];
+      a.ea.amax0 = am_rd(l - 1);
       a.ea.ldo = wp[l];
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_rbwd_l%d", l);
@@ -854,10 +920,10 @@ struct trpo_engine {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
       if (l == 0)
-        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1]}, WSeg{}, 0, skip, tag);
+        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1], am_x(), am_rd(0)}, WSeg{}, 0, skip, tag);
       else
-        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1]}, WSeg{H[l], RD[l], wp[l], wp[l + 1]}, 1,
-                    skip, tag);
+        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)},
+                    WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
     }
     reduce_grad(out, skip);
   }
@@ -903,14 +969,25 @@ struct trpo_engine {
       launch_fvp_chain(ca, chain_otm, stream);
       check_launch();
     }
+    if (f16) {
+      // the chain writes RH / RD without running maxima; the split weight gradients need them
+      am_reset(am_rh(0), L);
+      am_reset(am_rd(0), L);
+      for (int l = 0; l < L; ++l) {
+        if (l >= 1) launch_amax(RH[l], n, w[l], wp[l], am_rh(l), stream);
+        launch_amax(RD[l], n, w[l + 1], wp[l + 1], am_rd(l), stream);
+      }
+      check_launch();
+    }
     // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
     for (int l = 0; l < L; ++l) {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
       if (l == 0)
-        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1]}, WSeg{}, 0, skip, tag);
+        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1], am_x(), am_rd(0)}, WSeg{}, 0, skip, tag);
       else
-        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1]}, WSeg{H[l], RD[l], wp[l], wp[l + 1]}, 1, skip, tag);
+        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)},
+                    WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
     }
     reduce_grad(out, skip);
   }
@@ -937,7 +1014,7 @@ struct trpo_engine {
   // loss(th) at a device parameter vector, without touching the prepared cache
   void eval_losses_dev(const float* th) {
     require_batch();
-    PackArgs pa = pack_args(WFt, nullptr);
+    PackArgs pa = pack_args(WFt, nullptr, 2);
     launch_pack(pa, th, 0, nullptr, stream);
     split_parts(true, false, false, false, WFt, WFt3, nullptr, "split_t");
     forward(WFt, WFt3, th, RH, RowEpi::kLossHead, "ls_fwd");
@@ -1186,6 +1263,7 @@ int trpo_set_batch(trpo_engine* e, int64_t n, int64_t n_global, const float* sta
     };
     stage(states, obs, e->wp[0], e->X);
     stage(old_dist, A, e->wp[e->L], e->old);
+    e->update_x_amax();
     const int64_t* acts = actions;
     if (mem != TRPO_MEM_DEVICE) {
       e->copy_in(e->stage, actions, (size_t)n * sizeof(int64_t), mem);
@@ -1532,6 +1610,7 @@ int trpo_rollout_to_batch(trpo_engine* e, int64_t n_global) {
     e->rollout_compact(o);
     e->n = N;
     e->n_global = n_global;
+    e->update_x_amax();
     e->set_splits();
     e->prepared = false;
     e->have_rewards = true;
@@ -1739,6 +1818,7 @@ static int* option_slot(const std::string& k) {
   if (k == "split_mfma") return &g_options.split_mfma;
   if (k == "split_wg") return &g_options.split_wg;
   if (k == "chain") return &g_options.chain;
+  if (k == "split_f16") return &g_options.split_f16;
   throw ArgError("unknown option " + k);
 }
 

@@ -25,6 +25,10 @@
 #include <stdexcept>
 #include <string>
 
+#ifndef TRPO_EPI_TRACK
+#define TRPO_EPI_TRACK 1   // ablation builds only (tools): 0 drops the f16 running-max tracking
+#endif
+
 namespace trpo {
 
 static int env_int(const char* name, int dflt) {
@@ -33,7 +37,7 @@ static int env_int(const char* name, int dflt) {
 }
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
-                     env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1)};
+                     env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1)};
 
 namespace {
 
@@ -55,6 +59,36 @@ __device__ __forceinline__ float hmax32(float v) {
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 32));
   return v;
+}
+
+// workgroup max of v[i] >= 0 for the non-NULL slots, one atomicMax per slot per workgroup (float bits
+// order as unsigned for v >= 0) into the slot's counter for this block (kernels.h, kAmaxSub).
+// Every thread of the block must call it.
+__device__ __forceinline__ void amax_commit3(unsigned* s0, float v0, unsigned* s1, float v1, unsigned* s2, float v2) {
+  if (!s0 && !s1 && !s2) return;
+  __shared__ float red[3][16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    v0 = fmaxf(v0, __shfl_xor(v0, off, 64));
+    v1 = fmaxf(v1, __shfl_xor(v1, off, 64));
+    v2 = fmaxf(v2, __shfl_xor(v2, off, 64));
+  }
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wave] = v0;
+    red[1][wave] = v1;
+    red[2][wave] = v2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned* slot = threadIdx.x == 0 ? s0 : (threadIdx.x == 1 ? s1 : s2);
+    if (slot) {
+      float m = 0.0f;
+      for (int w = 0; w < nw; ++w) m = fmaxf(m, red[threadIdx.x][w]);
+      const unsigned bid = blockIdx.x + blockIdx.y * 7919u + blockIdx.z * 104729u;
+      if (m > 0.0f) atomicMax(slot + (bid % kAmaxSub) * kAmaxStride, __float_as_uint(m));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -126,7 +160,7 @@ __device__ __forceinline__ void epi_store(const RowEpiArgs& e, size_t idx, float
 // ---------------------------------------------------------------------------
 template <int EPI>
 __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowvalid, int col, int A,
-                                        float v) {
+                                        float v, float& m0, float& m1, float& m2) {
   // `row` is already clamped into [0, M); loads go to clamped (valid) addresses
   // unconditionally and are masked by selects, so hipcc keeps them in flight.
   const bool real = col < A;
@@ -175,6 +209,8 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
       if (st) {
         e.out1[sidx] = (float)dl;
         e.out2[sidx] = (float)ds;
+        m1 = fmaxf(m1, fabsf((float)dl));
+        m2 = fmaxf(m2, fabsf((float)ds));
       }
     }
   } else if constexpr (EPI == (int)RowEpi::kRHead) {
@@ -194,7 +230,10 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     const double spB = hsum32d(pd * B);
     const double sRAB = hsum32d(Rp * Aa * B);
     const double rd = e.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
-    if (st) e.out0[(size_t)row * e.ldo + col] = real ? (float)rd : 0.0f;
+    if (st) {
+      e.out0[(size_t)row * e.ldo + col] = real ? (float)rd : 0.0f;
+      if (real) m0 = fmaxf(m0, fabsf((float)rd));
+    }
   }
 }
 
@@ -219,6 +258,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int M = args.M;
   const RowEpiArgs& e = args.ea;
+  float mx0 = 0.0f, mx1 = 0.0f, mx2 = 0.0f;   // max |stored output| for the f16 operand scales
   if constexpr (epi_is_head(EPI)) {
     static_assert(WN == 1 && TN == 1, "row-wise head epilogue needs the whole row in one wave half");
     const int col = n0 + lr;
@@ -227,7 +267,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r]);
+        epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r], mx0, mx1, mx2);
       }
   } else {
     const bool fulln = (n0 + BN <= args.Npad);
@@ -293,6 +333,13 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
             } else {
               o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
             }
+            // running max for the f16 operand scales (rows past M -- dropped stores -- hold 0 or,
+            // for kRHidden, the tangent bias: harmless in a max)
+            if constexpr (TRPO_EPI_TRACK && EPI != (int)RowEpi::kTanh && EPI != (int)RowEpi::kRelu &&
+                          EPI != (int)RowEpi::kReluBwd) {
+              mx0 = fmaxf(mx0, fabsf(o0[r]));
+              if constexpr (EPI == (int)RowEpi::kPrepBwd) mx1 = fmaxf(mx1, fabsf(o1[r]));
+            }
           }
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -319,14 +366,17 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
           for (int r = 0; r < 16; ++r) {
             const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
             if (row < M && colv) {
-              float o0, o1;
+              float o0, o1 = 0.0f;
               epi_elem_v<EPI>(e, (size_t)row * e.ldo + colc, real, acc[tm][tn][r], real ? bv : 0.0f, o0, o1);
               epi_store<EPI>(e, (size_t)row * e.ldo + col, o0, o1);
+              mx0 = fmaxf(mx0, fabsf(o0));
+              mx1 = fmaxf(mx1, fabsf(o1));
             }
           }
       }
     }
   }
+  amax_commit3(e.amax0, mx0, e.amax1, mx1, e.amax2, mx2);
 }
 
 template <int WM, int WN, int TM, int TN, int BK, int EPI, int PF = 1>
@@ -514,18 +564,54 @@ __device__ __forceinline__ void split3(float x, unsigned short& h, unsigned shor
   l = bf16_bits(r2);
 }
 
+// f16 split (RowGemmArgs::f16): x (already scaled into [2^11, 2^12) by a power of two, see
+// f16_scale_exp) = h + l + O(2^-22 |x|) with h = f16(x), l = f16(x - h) (the difference is exact);
+// a*b ~= ah bh + (ah bl + al bh), the dropped al bl is ~2^-22 relative.  f16 MFMA runs at the bf16
+// rate, so 3 products instead of 6 halve the MFMA work; the scales keep every piece a normal f16
+// down to 2^-15 of the operand's max (below that the error is absolute, 2^-36 of the max).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split2h(float x, unsigned short& h, unsigned short& l) {
+  const _Float16 hh = (_Float16)x;
+  const _Float16 ll = (_Float16)(x - (float)hh);
+  h = __builtin_bit_cast(unsigned short, hh);
+  l = __builtin_bit_cast(unsigned short, ll);
+}
+// the slot's max (over its kAmaxSub counters, kAmaxSub / 64 per lane) -> scale exponent; all lanes of
+// the wave must call it
+__device__ __forceinline__ int amax_exp(const unsigned* amax) {
+  if (!amax) return f16_scale_exp(1.0f);
+  const int lane = threadIdx.x & 63;
+  float v = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kAmaxSub / 64; ++i) v = fmaxf(v, __uint_as_float(amax[(lane + 64 * i) * kAmaxStride]));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return f16_scale_exp(v);
+}
+template <int TM, int TN>
+__device__ __forceinline__ void scale_acc(f32x16 (&acc)[TM][TN], int e) {
+  if (e == 0) return;
+  const float f = __builtin_ldexpf(1.0f, e);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= f;
+}
+
 // LDS images are [row][16 k] bf16 (32-B rows, no padding); the two 16-B k-chunks of
 // a row swap places on odd 8-row groups, so the 16 lanes of a ds_read_b128 phase
 // (rows r..r+15, one chunk) hit 16 distinct bank groups.
 __device__ __forceinline__ int swz16(int row, int chunk) { return row * 16 + ((chunk ^ ((row >> 3) & 1)) << 3); }
 
-template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF>
+template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF, int NP>
 __global__ void __launch_bounds__(WM* WN * 64, OCC)   // OCC waves / SIMD
 rowgemm3_kernel(const RowGemmArgs args) {
+  // NP = 3: bf16 hi/mid/lo planes, 6 products ; NP = 2: scaled f16 hi/lo planes, 3 products
   constexpr int BK = 16;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int APL = BM * BK, BPL = BN * BK;     // one plane
-  constexpr int STG = 3 * (APL + BPL);
+  constexpr int STG = NP * (APL + BPL);
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STG];
   if (args.skip && *args.skip) return;
 
@@ -540,6 +626,17 @@ rowgemm3_kernel(const RowGemmArgs args) {
   const int nt0 = (args.seg[0].K + BK - 1) / BK;
   const int nt1 = args.nseg > 1 ? (args.seg[1].K + BK - 1) / BK : 0;
   const int ntiles = nt0 + nt1;
+  // f16: per-segment operand scales 2^eA, 2^eB (products scaled by 2^(eA+eB))
+  int eA0 = 0, eP0 = 0, eA1 = 0, eP1 = 0;
+  if constexpr (NP == 2) {
+    eA0 = amax_exp(args.seg[0].amaxA);
+    eP0 = eA0 + amax_exp(args.seg[0].amaxB);
+    if (args.nseg > 1) {
+      eA1 = amax_exp(args.seg[1].amaxA);
+      eP1 = eA1 + amax_exp(args.seg[1].amaxB);
+    }
+  }
+  const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -548,15 +645,17 @@ rowgemm3_kernel(const RowGemmArgs args) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   constexpr int AF4 = BM * BK / 4;          // f32x4 of A per k-tile
-  constexpr int BC = 3 * BN * (BK / 8);     // 16-B chunks of B planes per k-tile
+  constexpr int BC = NP * BN * (BK / 8);    // 16-B chunks of B planes per k-tile
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BC + NT - 1) / NT;
   struct Stage {
     f32x4 ra[AP];
     u16x8 rb[BP];
     bool oka[AP], okb[BP];
+    bool s1;
   };
   auto gload = [&](Stage& st, int t) {
     const bool s1 = t >= nt0;
+    st.s1 = s1;
     const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
     const float* Ap = sg.A;
     const int lda = sg.lda, K = sg.K;
@@ -584,26 +683,40 @@ rowgemm3_kernel(const RowGemmArgs args) {
   };
   auto sstore = [&](const Stage& st, int buf) {
     unsigned short* As = smem + buf * STG;
-    unsigned short* Bs = As + 3 * APL;
+    unsigned short* Bs = As + NP * APL;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
       if (AF4 % NT == 0 || f < AF4) {
         const int r = f / (BK / 4), kq = f % (BK / 4);
         const f32x4 x = st.oka[i] ? st.ra[i] : f32x4{};
-        u16x4 h, m, l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          unsigned short hh, mm, ll;
-          split3(x[j], hh, mm, ll);
-          h[j] = hh;
-          m[j] = mm;
-          l[j] = ll;
-        }
         unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
-        *reinterpret_cast<u16x4*>(dst) = h;
-        *reinterpret_cast<u16x4*>(dst + APL) = m;
-        *reinterpret_cast<u16x4*>(dst + 2 * APL) = l;
+        if constexpr (NP == 3) {
+          u16x4 h, m, l;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned short hh, mm, ll;
+            split3(x[j], hh, mm, ll);
+            h[j] = hh;
+            m[j] = mm;
+            l[j] = ll;
+          }
+          *reinterpret_cast<u16x4*>(dst) = h;
+          *reinterpret_cast<u16x4*>(dst + APL) = m;
+          *reinterpret_cast<u16x4*>(dst + 2 * APL) = l;
+        } else {
+          const float sa = st.s1 ? sA1 : sA0;
+          u16x4 h, l;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned short hh, ll;
+            split2h(x[j] * sa, hh, ll);
+            h[j] = hh;
+            l[j] = ll;
+          }
+          *reinterpret_cast<u16x4*>(dst) = h;
+          *reinterpret_cast<u16x4*>(dst + APL) = l;
+        }
       }
     }
 #pragma unroll
@@ -618,30 +731,55 @@ rowgemm3_kernel(const RowGemmArgs args) {
   };
   auto compute = [&](int buf) {
     const unsigned short* As = smem + buf * STG;
-    const unsigned short* Bs = As + 3 * APL;
+    const unsigned short* Bs = As + NP * APL;
     // fragments streamed per output column tile to keep few registers live
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      bf16x8 b[3];
       const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
+      if constexpr (NP == 3) {
+        bf16x8 b[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
+        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        bf16x8 a[3];
-        const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+        for (int tm = 0; tm < TM; ++tm) {
+          bf16x8 a[3];
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
-        // smallest terms first
-        f32x16 c = acc[tm][tn];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
-        acc[tm][tn] = c;
+          for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
+          // smallest terms first
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
+      } else {
+        f16x8 b[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) b[p] = *reinterpret_cast<const f16x8*>(Bs + p * BPL + bo);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          f16x8 a[2];
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+#pragma unroll
+          for (int p = 0; p < 2; ++p) a[p] = *reinterpret_cast<const f16x8*>(As + p * APL + ao);
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
       }
+    }
+  };
+  // f16: when the k-tiles move from segment 0 to segment 1, bring the accumulator to segment 1's
+  // product scale (powers of two: exact)
+  auto seg_switch = [&](int t) {
+    if constexpr (NP == 2) {
+      if (t == nt0 && nt1 > 0) scale_acc<TM, TN>(acc, eP1 - eP0);
     }
   };
 
@@ -653,6 +791,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
       lds_barrier();
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
+        seg_switch(t);
         compute(t & 1);
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
         lds_barrier();
@@ -667,17 +806,23 @@ rowgemm3_kernel(const RowGemmArgs args) {
       int t = 0;
       for (; t + 1 < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
+        seg_switch(t);
         compute(0);
         sstore(S1, 1);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+        seg_switch(t + 1);
         compute(1);
         if (t + 2 < ntiles) sstore(S0, 0);
         lds_barrier();
       }
-      if (t < ntiles) compute(0);
+      if (t < ntiles) {
+        seg_switch(t);
+        compute(0);
+      }
     }
   }
+  if constexpr (NP == 2) scale_acc<TM, TN>(acc, -(nt1 > 0 ? eP1 : eP0));
   row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
 }
 
@@ -689,13 +834,13 @@ rowgemm3_kernel(const RowGemmArgs args) {
 // column and 8 consecutive rows (8 coalesced dword loads), splits them and
 // writes one 16-B k-chunk per plane of the [column][16 rows] LDS image.
 // ---------------------------------------------------------------------------
-template <int WM, int WN, int TM, int TN, int OCC, int PF>
+template <int WM, int WN, int TM, int TN, int OCC, int PF, int NP>
 __global__ void __launch_bounds__(WM* WN * 64, OCC)
 wgrad3_kernel(const WGradArgs args) {
   constexpr int BK = 16;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int APL = BM * BK, BPL = BN * BK;
-  constexpr int STG = 3 * (APL + BPL);
+  constexpr int STG = NP * (APL + BPL);
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STG];
   __shared__ float cs_sh[2][BN];
   if (args.skip && *args.skip) return;
@@ -709,6 +854,14 @@ wgrad3_kernel(const WGradArgs args) {
   const int nk = r1 > r0 ? (r1 - r0 + BK - 1) / BK : 0;
   const int ntiles = nk * args.nseg;
   const bool do_colsum = (blockIdx.x == 0);
+  // f16: operand scales per segment (see rowgemm3_kernel)
+  int eA[2] = {0, 0}, eB[2] = {0, 0};
+  if constexpr (NP == 2) {
+    for (int g = 0; g < args.nseg && g < 2; ++g) {
+      eA[g] = amax_exp(args.seg[g].amaxA);
+      eB[g] = amax_exp(args.seg[g].amaxB);
+    }
+  }
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -725,6 +878,7 @@ wgrad3_kernel(const WGradArgs args) {
     float va[AP][8], vb[BP][8];
     int nv;          // valid rows of the tile (>= 16: all)
     bool cs;         // this tile belongs to the column-summed segment
+    int sg;          // segment
   };
   auto gload = [&](Stage& st, int t) {
     const int sg = t / nk;
@@ -736,6 +890,7 @@ wgrad3_kernel(const WGradArgs args) {
     const int rb0 = r0 + kt * BK;
     st.nv = r1 - rb0;
     st.cs = do_colsum && sg == args.colsum_seg;
+    st.sg = sg;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
@@ -761,32 +916,47 @@ wgrad3_kernel(const WGradArgs args) {
       }
     }
   };
-  auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int nv) {
-    u16x8 h, m, l;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float x = (8 * g + q < nv) ? v[q] : 0.0f;
-      unsigned short hh, mm, ll;
-      split3(x, hh, mm, ll);
-      h[q] = hh;
-      m[q] = mm;
-      l[q] = ll;
-    }
+  auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int nv, int e) {
     unsigned short* dst = base + swz16(c, g);
-    *reinterpret_cast<u16x8*>(dst) = h;
-    *reinterpret_cast<u16x8*>(dst + plane_elems) = m;
-    *reinterpret_cast<u16x8*>(dst + 2 * plane_elems) = l;
+    if constexpr (NP == 2) {
+      const float sc = __builtin_ldexpf(1.0f, e);
+      u16x8 h, l;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = (8 * g + q < nv) ? v[q] : 0.0f;
+        unsigned short hh, ll;
+        split2h(x * sc, hh, ll);
+        h[q] = hh;
+        l[q] = ll;
+      }
+      *reinterpret_cast<u16x8*>(dst) = h;
+      *reinterpret_cast<u16x8*>(dst + plane_elems) = l;
+    } else {
+      u16x8 h, m, l;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = (8 * g + q < nv) ? v[q] : 0.0f;
+        unsigned short hh, mm, ll;
+        split3(x, hh, mm, ll);
+        h[q] = hh;
+        m[q] = mm;
+        l[q] = ll;
+      }
+      *reinterpret_cast<u16x8*>(dst) = h;
+      *reinterpret_cast<u16x8*>(dst + plane_elems) = m;
+      *reinterpret_cast<u16x8*>(dst + 2 * plane_elems) = l;
+    }
   };
   auto sstore = [&](const Stage& st, int buf) {
     unsigned short* As = smem + buf * STG;
-    unsigned short* Bs = As + 3 * APL;
+    unsigned short* Bs = As + NP * APL;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
       if (AI % NT == 0 || f < AI) {
         const int c = f % BM, g = f / BM;
         // an invalid column holds finite clamped data; zero it through nv = 0
-        put(As, APL, c, g, st.va[i], m0 + c < args.Mpad ? st.nv : 0);
+        put(As, APL, c, g, st.va[i], m0 + c < args.Mpad ? st.nv : 0, eA[st.sg]);
       }
     }
 #pragma unroll
@@ -795,7 +965,7 @@ wgrad3_kernel(const WGradArgs args) {
       if (BI % NT == 0 || f < BI) {
         const int c = f % BN, g = f / BN;
         const int nv = n0 + c < args.Npad ? st.nv : 0;
-        put(Bs, BPL, c, g, st.vb[i], nv);
+        put(Bs, BPL, c, g, st.vb[i], nv, eB[st.sg]);
         if (st.cs) {
           float cs = 0.0f;
 #pragma unroll
@@ -807,28 +977,51 @@ wgrad3_kernel(const WGradArgs args) {
   };
   auto compute = [&](int buf) {
     const unsigned short* As = smem + buf * STG;
-    const unsigned short* Bs = As + 3 * APL;
+    const unsigned short* Bs = As + NP * APL;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      bf16x8 b[3];
       const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
+      if constexpr (NP == 3) {
+        bf16x8 b[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
+        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        bf16x8 a[3];
-        const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+        for (int tm = 0; tm < TM; ++tm) {
+          bf16x8 a[3];
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
-        f32x16 c = acc[tm][tn];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
-        acc[tm][tn] = c;
+          for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
+      } else {
+        f16x8 b[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) b[p] = *reinterpret_cast<const f16x8*>(Bs + p * BPL + bo);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          f16x8 a[2];
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+#pragma unroll
+          for (int p = 0; p < 2; ++p) a[p] = *reinterpret_cast<const f16x8*>(As + p * APL + ao);
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
       }
+    }
+  };
+  auto seg_switch = [&](int t) {
+    if constexpr (NP == 2) {
+      if (t == nk && args.nseg > 1) scale_acc<TM, TN>(acc, (eA[1] + eB[1]) - (eA[0] + eB[0]));
     }
   };
 
@@ -840,6 +1033,7 @@ wgrad3_kernel(const WGradArgs args) {
       lds_barrier();
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
+        seg_switch(t);
         compute(t & 1);
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
         lds_barrier();
@@ -853,16 +1047,25 @@ wgrad3_kernel(const WGradArgs args) {
       int t = 0;
       for (; t + 1 < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);
+        seg_switch(t);
         compute(0);
         sstore(S1, 1);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+        seg_switch(t + 1);
         compute(1);
         if (t + 2 < ntiles) sstore(S0, 0);
         lds_barrier();
       }
-      if (t < ntiles) compute(0);
+      if (t < ntiles) {
+        seg_switch(t);
+        compute(0);
+      }
     }
+  }
+  if constexpr (NP == 2) {
+    const int last = args.nseg > 1 ? 1 : 0;
+    scale_acc<TM, TN>(acc, -(eA[last] + eB[last]));
   }
 
   float* out = args.slab + (size_t)split * args.slab_stride;
@@ -900,7 +1103,25 @@ __global__ void __launch_bounds__(256) split_b_kernel(const SplitArgs a, const i
   const int f = blockIdx.x * 256 + threadIdx.x;
   // lanes run over columns first so the f32 reads of one k row coalesce
   const int n = f % j.Npad, c = f / j.Npad;
+  const float sb = a.f16 ? __builtin_ldexpf(1.0f, amax_exp(j.amax)) : 1.0f;   // whole wave, before any exit
   if (c >= nchunk) return;
+  const size_t plane = (size_t)j.Npad * j.ldk;
+  uint16_t* dst = j.B3 + (size_t)n * j.ldk + 8 * c;
+  if (a.f16) {
+    u16x8 h, l;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 8 * c + q;
+      const float x = k < j.K ? j.B[(size_t)k * j.ldb + n] : 0.0f;
+      unsigned short hh, ll;
+      split2h(x * sb, hh, ll);
+      h[q] = hh;
+      l[q] = ll;
+    }
+    *reinterpret_cast<u16x8*>(dst) = h;
+    *reinterpret_cast<u16x8*>(dst + plane) = l;
+    return;
+  }
   u16x8 h, m, l;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -912,8 +1133,6 @@ __global__ void __launch_bounds__(256) split_b_kernel(const SplitArgs a, const i
     m[q] = mm;
     l[q] = ll;
   }
-  const size_t plane = (size_t)j.Npad * j.ldk;
-  uint16_t* dst = j.B3 + (size_t)n * j.ldk + 8 * c;
   *reinterpret_cast<u16x8*>(dst) = h;
   *reinterpret_cast<u16x8*>(dst + plane) = m;
   *reinterpret_cast<u16x8*>(dst + 2 * plane) = l;
@@ -1101,7 +1320,12 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
     if (!a.seg[i].B3 || a.seg[i].ldk < ((a.seg[i].K + 15) / 16) * 16 || a.seg[i].ldk % 8)
       throw std::runtime_error("split-bf16 row GEMM: segment without B planes");
   const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
-  hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, s, a);
+  if (a.f16)
+    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 2>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 3>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
+                       s, a);
 }
 
 template <int EPI>
@@ -1118,6 +1342,8 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
       case 5: launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s); break;   // 256 x 256, 2 k-tiles in flight
       case 6: launch_row3_cfg<2, 4, 2, 2, EPI, 2, 2>(a, s); break;   // 128 x 256, 2 k-tiles in flight
       case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
+      case 8: launch_row3_cfg<2, 4, 2, 2, EPI, 4>(a, s); break;      // 128 x 256, 2 blocks / CU
+      case 9: launch_row3_cfg<2, 4, 2, 2, EPI, 4, 2>(a, s); break;   // 128 x 256, 2 blocks / CU, 2 in flight
       default: launch_row3_cfg<2, 4, 2, 2, EPI>(a, s); break;  // 128 x 256
     }
   } else {
@@ -1151,7 +1377,10 @@ void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   if (a.rows_per_split % 16) throw std::runtime_error("split-bf16 wgrad: rows_per_split % 16");
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
-  hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF>), grid, dim3(WM * WN * 64), 0, s, a);
+  if (a.f16)
+    hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 2>), grid, dim3(WM * WN * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 3>), grid, dim3(WM * WN * 64), 0, s, a);
 }
 
 }  // namespace

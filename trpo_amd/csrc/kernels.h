@@ -21,7 +21,22 @@ struct Options {
   int split_mfma;  // row GEMMs with N > 128 on bf16 MFMA with fp32 operands split 3 ways (hi+mid+lo)
   int split_wg;    // weight gradients with fan_out > 128 on the split-bf16 MFMA (tile choice 1..3)
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
+  int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
 };
+
+// A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
+// workgroup and atomicMax into counter (block id mod kAmaxSub), so the device-scope atomics of a
+// launch are few and spread; consumers take the max of the kAmaxSub counters (a few loads per lane).
+constexpr int kAmaxSub = 256, kAmaxStride = 32, kAmaxSlot = kAmaxSub * kAmaxStride;   // in unsigned
+
+// Power-of-two scale exponent for the f16 split: max|x| * 2^e lands in [2^11, 2^12).
+__host__ __device__ inline int f16_scale_exp(float m) {
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 0;
+  int q = 0;
+  (void)frexpf(m, &q);
+  int e = 12 - q;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
 extern Options g_options;
 
 // ---------------------------------------------------------------------------
@@ -31,10 +46,15 @@ struct GemmSeg {
   const float* A;  // [M][lda]
   const float* B;  // [K][ldb]
   int lda, ldb, K; // K multiple of 4
-  // split-bf16 GEMM only: B as three bf16 planes (hi, mid, lo) [3][Npad][ldk], k contiguous,
-  // zero for k >= K (see launch_split_b); plane = elements per plane
+  // split GEMM only: B as bf16 planes (hi, mid, lo) [3][Npad][ldk] or, with RowGemmArgs::f16,
+  // scaled f16 planes (hi, lo) [2][Npad][ldk]; k contiguous, zero for k >= K (launch_split_b);
+  // plane = elements per plane
   const uint16_t* B3 = nullptr;
   int ldk = 0, plane = 0;
+  // f16 split only: running max |A| / max |B| (float bits, atomicMax'd by their producers) that
+  // set the power-of-two operand scales; NULL means "bounded by 1"
+  const unsigned* amaxA = nullptr;
+  const unsigned* amaxB = nullptr;
 };
 
 enum class RowEpi : int {
@@ -68,6 +88,11 @@ struct RowEpiArgs {
   const float* adv;    // [M]
   double* rowterms;    // [M][4] (surr*N, kl*N, ent*N, -)
   double invN;         // 1 / N_global
+  // optional running max |out0| / |out1| / |out2| over the valid rows (float bits, atomicMax), the
+  // operand scales of the f16 split GEMMs that consume these outputs
+  unsigned* amax0 = nullptr;
+  unsigned* amax1 = nullptr;
+  unsigned* amax2 = nullptr;
 };
 
 struct RowGemmArgs {
@@ -77,6 +102,7 @@ struct RowGemmArgs {
   const int* skip;     // optional device flag: launch is a no-op when *skip != 0
   RowEpi epi;
   RowEpiArgs ea;
+  int f16 = 0;         // split path: 1 = two scaled f16 planes / 3 products, 0 = three bf16 planes / 6
 };
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
@@ -89,11 +115,13 @@ struct SplitJob {
   const float* B;
   uint16_t* B3;
   int K, Npad, ldb, ldk;
+  const unsigned* amax = nullptr;   // f16: max |B| (float bits) that sets the plane scale
 };
 constexpr int kMaxSplitJobs = 16;
 struct SplitArgs {
   int n;
   SplitJob job[kMaxSplitJobs];
+  int f16 = 0;
 };
 void launch_split_b(const SplitArgs& a, const int* skip, hipStream_t s);
 
@@ -106,6 +134,8 @@ struct WSeg {
   const float* A;  // [rows][lda]
   const float* B;  // [rows][ldb]
   int lda, ldb;
+  const unsigned* amaxA = nullptr;   // f16 split: max |A|, max |B| (float bits; NULL = bounded by 1)
+  const unsigned* amaxB = nullptr;
 };
 
 struct WGradArgs {
@@ -120,6 +150,7 @@ struct WGradArgs {
   int64_t slab_stride; // floats between consecutive splits
   int64_t off_w, off_b;
   const int* skip;
+  int f16 = 0;         // split path: scaled f16 (3 products) instead of bf16 (6 products)
 };
 
 void launch_wgrad(const WGradArgs& a, hipStream_t s);
@@ -132,6 +163,7 @@ struct LayerPack {
   int a, b, apad, bpad;
   float* WF;       // [2*apad][bpad]: rows [0,a) = W ; rows [apad, apad+a) = V
   float* WB;       // [2*bpad][apad]: rows [0,b) = W^T ; rows [bpad, bpad+b) = V^T
+  unsigned* amax = nullptr;   // optional: atomicMax of max |W_l| (float bits)
 };
 constexpr int kMaxLayers = 8;
 struct PackArgs {
@@ -219,6 +251,8 @@ void launch_axpby(float* y, const float* x, float alpha, float beta, int64_t n, 
 void launch_scale_copy(const float* x, float* y, float alpha, int64_t n, hipStream_t s);          // y = alpha*x
 void launch_i64_to_i32(const int64_t* src, int* dst, int64_t n, int* bad, int hi, hipStream_t s);
 void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s);
+// out = max(out, max |A[r][c]|) over r < n, c < w (float bits via atomicMax)
+void launch_amax(const float* A, int64_t n, int w, int ld, unsigned* out, hipStream_t s);
 void launch_copy_rows(const float* src, int64_t n, int w, int ld_src, float* dst, int ld_dst, hipStream_t s);
 
 // ---------------------------------------------------------------------------

@@ -20,18 +20,41 @@ namespace trpo {
 
 namespace {
 
+// wave max of v >= 0 -> one atomicMax per wave (float bits order as unsigned for v >= 0)
+__device__ __forceinline__ void amax_wave_commit(unsigned* slot, float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  const unsigned wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) + blockIdx.y * 7919u;
+  if ((threadIdx.x & 63) == 0 && v > 0.0f) atomicMax(slot + (wid % kAmaxSub) * kAmaxStride, __float_as_uint(v));
+  // (few blocks: per-wave atomics are fine here)
+}
+
 __global__ void pack_kernel(const PackArgs pa, const float* src, int which, const int* skip) {
   if (skip && *skip) return;
   const LayerPack& L = pa.L[blockIdx.y];
   const int64_t n = (int64_t)L.a * L.b;
   const float* w = src + L.off_w;
+  float mx = 0.0f;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(e / L.b), j = (int)(e % L.b);
     const float v = w[e];
+    mx = fmaxf(mx, fabsf(v));
     L.WF[(int64_t)(which ? L.apad + i : i) * L.bpad + j] = v;
     if (L.WB) L.WB[(int64_t)(which ? L.bpad + j : j) * L.apad + i] = v;
   }
+  if (L.amax) amax_wave_commit(L.amax, mx);
+}
+
+__global__ void amax_kernel(const float* A, int64_t n, int w, int ld, unsigned* out) {
+  float mx = 0.0f;
+  const int64_t tot = n * w;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / w;
+    const int c = (int)(e - r * w);
+    mx = fmaxf(mx, fabsf(A[r * ld + c]));
+  }
+  amax_wave_commit(out, mx);
 }
 
 __global__ void reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* out,
@@ -456,6 +479,11 @@ void launch_scale_copy(const float* x, float* y, float alpha, int64_t n, hipStre
 
 void launch_i64_to_i32(const int64_t* src, int* dst, int64_t n, int* bad, int hi, hipStream_t s) {
   hipLaunchKernelGGL(i64_to_i32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n, bad, hi);
+}
+
+void launch_amax(const float* A, int64_t n, int w, int ld, unsigned* out, hipStream_t s) {
+  if (n <= 0 || w <= 0) return;
+  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n * w, 256, 2048)), dim3(256), 0, s, A, n, w, ld, out);
 }
 
 void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
