@@ -18,11 +18,14 @@ Default workload (N=1 and the scaling runs): C4 = 8,000,000 states, obs 128,
 states are split row-wise (path-aligned), so ``scaling`` is "strong".
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel (largest
-share of HIP-event time over the timed region, on the engine's stream):
-algorithmic FLOPs per launch / average launch time vs the ceiling of the MFMA
-path that kernel runs on -- the f32 MFMA peak (157.3 TF/s), or for the
-split-bf16 GEMMs (fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMA
-products per fp32 product) the bf16 dense peak / 6 = 416.7 TF/s of fp32 work.
+share of HIP-event time over the timed region, on the engine's stream) against
+the roof that bounds it: its algorithmic FLOPs at the ceiling of its MFMA path
+-- the f32 MFMA peak (157.3 TF/s), or for the split GEMMs (fp32 operands scaled
+and split into f16 hi+lo pieces, 3 MFMA products per fp32 product) the f16 dense
+peak / 3 = 833.3 TF/s of fp32 work (bf16 hi+mid+lo, 6 products: / 6) -- versus
+its algorithmic HBM bytes (every operand read once, every output written once)
+at 8 TB/s; the larger time is the bound ("mfma" or "hbm"), and `achieved` /
+`peak` are in that roof's unit.
 ``traffic`` is the HBM bytes per launch of that kernel measured by rocprofv3
 FETCH_SIZE / WRITE_SIZE passes of this same command (tools/prof.sh ->
 tools/pmc_traffic.py -> profiles/<round>/traffic.json), when a committed file
@@ -47,9 +50,17 @@ sys.path.insert(0, ROOT)
 
 METRIC = "TRPO updates/sec (10-iter CG + linesearch) at N states; FVP GB/s vs HBM peak"
 PEAK_F32_TFLOPS = 157.3        # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
-PEAK_BF16_TFLOPS = 2500.0      # MI355X_MICROARCH.md: BF16 MFMA dense peak
-SPLIT_PRODUCTS = 6             # hh, hm, mh, hl, lh, mm per fp32 product
-PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / SPLIT_PRODUCTS
+PEAK_BF16_TFLOPS = 2500.0      # MI355X_MICROARCH.md: BF16 / F16 MFMA dense peak
+
+
+def split_products() -> int:
+    """MFMA products per fp32 product on the split path: f16 hi+lo (hh, hl, lh) or bf16 hi+mid+lo."""
+    from trpo_amd._lib import get_option
+    return 3 if get_option("split_f16") else 6
+
+
+def peak_split_tflops() -> float:
+    return PEAK_BF16_TFLOPS / split_products()
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_LEN = 200              # CartPole-v0 cap (SURVEY.md §8(d))
 
@@ -119,7 +130,46 @@ def tag_is_split(tag: str, widths) -> bool:
 
 
 def tag_peak(tag: str, widths) -> float:
-    return PEAK_SPLIT_TFLOPS if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
+    return peak_split_tflops() if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
+
+
+def tag_bytes(tag: str, widths, n: int) -> float:
+    """Algorithmic HBM bytes of one launch: each activation operand read once and each output written
+    once (f32, real widths; weights and slabs are O(P) and left out)."""
+    role, _, l = tag.rpartition("_l")
+    if not l.isdigit():
+        return 0.0
+    l = int(l)
+    L = len(widths) - 1
+    w = widths
+    cols = 0
+    if role == "fvp_rfwd":
+        if l == 0:
+            cols = w[0] + 2 * w[1]                          # X ; H1 (epilogue) ; RH1 out
+        elif l < L - 1:
+            cols = 2 * w[l] + 2 * w[l + 1]                  # RH_l, H_l ; H_{l+1} ; RH_{l+1} out
+        else:
+            cols = 2 * w[l] + 2 * w[l + 1]                  # RH, H ; P ; RD_L out
+    elif role == "fvp_rbwd":
+        cols = 2 * w[l + 1] + 4 * w[l]                      # RD_l, D_l ; H_l, E, RH_l ; RD_{l-1} out
+    elif role == "fvp_wgrad":
+        cols = w[0] + w[1] if l == 0 else 2 * w[l] + 2 * w[l + 1]
+    elif role in ("fwd", "ls_fwd"):
+        cols = w[l] + w[l + 1] + (2 * w[l + 1] if l == L - 1 else 0)
+    elif role == "bwd":
+        cols = w[l + 1] + 3 * w[l]                          # D_l ; H ; D, E out
+    elif role == "pg_bwd":
+        cols = w[l + 1] + 2 * w[l]
+    elif role == "pg_wgrad":
+        cols = w[l] + w[l + 1]
+    return 4.0 * n * cols
+
+
+def tag_roof(tag: str, widths, n: int):
+    """(bound, seconds at the roof) of one launch."""
+    t_mfma = tag_flops(tag, widths, n) / (tag_peak(tag, widths) * 1e12)
+    t_hbm = tag_bytes(tag, widths, n) / (PEAK_HBM_GBS * 1e9)
+    return ("hbm", t_hbm) if t_hbm > t_mfma else ("mfma", t_mfma)
 
 
 def committed_traffic(config: str, rows: int, tag: str):
@@ -285,12 +335,18 @@ def main():
         cnt, tot_ms = kernel_tags[dom]
         avg_s = tot_ms / cnt / 1e3
         fl = tag_flops(dom, widths, n)
-        achieved = fl / avg_s / 1e12
-        peak = tag_peak(dom, widths)
+        by = tag_bytes(dom, widths, n)
+        bound, _ = tag_roof(dom, widths, n)
+        if bound == "hbm":
+            achieved, peak, unit = by / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+            peak_basis = "HBM3E 8.0 TB/s"
+        else:
+            achieved, peak, unit = fl / avg_s / 1e12, tag_peak(dom, widths), "TFLOP/s"
+            peak_basis = ("split MFMA: f16/bf16 dense peak / %d products" % split_products()
+                          if tag_is_split(dom, widths) else "f32 MFMA peak")
         upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / args.steps
-        # seconds one update would take with every kernel at its path's peak
-        upd_peak_s = sum(tag_flops(t, widths, n) * c / (tag_peak(t, widths) * 1e12)
-                         for t, (c, _) in kernel_tags.items()) / args.steps
+        # seconds one update would take with every kernel at its own roof (max of MFMA and HBM time)
+        upd_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / args.steps
         tr = committed_traffic(args.config, N, dom) if world == 1 else None
         upd_s = elapsed / args.steps
         fvp_ms = sum(ms for t, (c, ms) in prof.items() if t.startswith("fvp_") or t == "reduce")
@@ -309,9 +365,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "arithmetic": "fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on bf16 MFMA with "
-                          "each fp32 operand split exactly into hi+mid+lo bf16 pieces (6 products, error below "
-                          "f32 MFMA's); narrower GEMMs on f32 MFMA; softmax heads and CG scalars in f64",
+            "arithmetic": ("fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on f16 MFMA with each "
+                           "fp32 operand scaled by a power of two and split into hi+lo f16 pieces (3 products, "
+                           "error 2^-22 relative)" if split_products() == 3 else
+                           "fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on bf16 MFMA with "
+                           "each fp32 operand split exactly into hi+mid+lo bf16 pieces (6 products)") +
+                          "; narrower GEMMs on f32 MFMA; softmax heads and CG scalars in f64",
             "data": "synthetic (X~N(0,1), a~U{0..A-1}, rewards~U(0,1), paths of 200 steps, "
                     "random-init policy, pi_old = p(theta_0))",
             "config": {"workload": cfg["name"] + "; full update = discount+standardise+pg+10 CG+shs FVP+"
@@ -319,17 +378,20 @@ def main():
                        "n_states": N, "obs_dim": cfg["obs"], "hidden": cfg["hidden"], "n_actions": cfg["A"],
                        "num_params": eng.num_params, "cg_iters": 10, "residual_tol": 0.0,
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
-                         "unit": "TFLOP/s", "frac": achieved / peak,
+            "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak,
                          "traffic": tr[1]["traffic_bytes"] if tr else None,
-                         "peak_basis": ("split-bf16 MFMA: bf16 dense peak / 6 products" if peak == PEAK_SPLIT_TFLOPS
-                                        else "f32 MFMA peak"),
+                         "peak_basis": peak_basis,
+                         "algorithmic_bytes_per_launch": by, "flops_per_launch": fl,
+                         "mfma_tflops": fl / avg_s / 1e12, "mfma_peak": tag_peak(dom, widths),
+                         "hbm_gbs_algorithmic": by / avg_s / 1e9,
                          "hbm_gbs_at_traffic": tr[1]["traffic_bytes"] / avg_s / 1e9 if tr else None,
                          "traffic_source": tr[0] if tr else None,
-                         "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt},
+                         "avg_launch_ms": avg_s * 1e3, "launches": cnt},
             "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
                                 "achieved_tflops": upd_flops * world / upd_s / 1e12,
-                                "frac_of_peak": upd_peak_s / upd_s},
+                                "roof_ms_per_update": upd_peak_s * 1e3,
+                                "frac_of_roof": upd_peak_s / upd_s},
             "fvp": {"ms_per_fvp": fvp_s * 1e3, "gbps_algorithmic": fvp_bytes / fvp_s / 1e9,
                     "hbm_frac": fvp_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
                     "tflops": fvp_flops_per_row(widths) * n / fvp_s / 1e12},

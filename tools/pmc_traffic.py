@@ -19,17 +19,19 @@ import os
 import statistics
 
 # tag -> (kernel-name substring, period, phase): the phase-th of every `period` dispatches
+# (kernel template arguments as rocprofv3 prints them; the last rowgemm3/wgrad3 argument is the
+# plane count: 2 = the default f16 split)
 SPECS = {
-    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2>", 2, 1),
-    "fvp_rbwd_l2": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2>", 2, 0),
-    "fvp_rfwd_l0": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2>", 2, 0),
-    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2>", 2, 1),
+    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 2, 1),
+    "fvp_rbwd_l2": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 2, 0),
+    "fvp_rfwd_l0": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 0),
+    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 1),
     "fvp_rfwd_l2": ("rowgemm_kernel<4, 1, 2, 1, 16, 7, 1>", 1, 0),
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
-    "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 2>",
-    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 2>",
+    "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 2, 2>",
+    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 2, 2>",
     "fvp_wgrad_l2": "wgrad_kernel<4, 1, 2, 1, 16, 1>",
 }
 
