@@ -969,7 +969,9 @@ struct trpo_engine {
       launch_fvp_chain(ca, chain_otm, stream);
       check_launch();
     }
-    if (f16) {
+    bool split_wg_used = false;   // a weight gradient on the split path reads RH / RD scales
+    for (int l = 0; l < L; ++l) split_wg_used |= g_options.split_wg != 0 && w[l + 1] > 128;
+    if (f16 && split_wg_used) {
       // the chain writes RH / RD without running maxima; the split weight gradients need them
       am_reset(am_rh(0), L);
       am_reset(am_rd(0), L);

@@ -1313,6 +1313,228 @@ void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
 
 int wide_cfg() { return g_options.row_cfg; }
 
+// One global_load_lds_dwordx4 as inline asm: 16 B per lane from `src` into LDS at the wave-uniform
+// byte address `lds` + 16 * lane.  Opaque to hipcc's s_waitcnt bookkeeping (the builtin form makes
+// hipcc drain vmcnt(0) before every later LDS read), so the caller counts completion itself.
+__device__ __forceinline__ void glds16(const void* src, const void* lds) {
+  unsigned keep;
+  const unsigned dst = (unsigned)(uintptr_t)lds;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA pipelined f16 split row GEMM (split_mfma = 10).  Same tile as config 5
+// (256 x 256, 8 waves as 4 x 2, 2 x 4 accumulators per wave) and the same
+// arithmetic as rowgemm3_kernel<.., NP = 2>, but the operands stream straight
+// into LDS with global_load_lds_dwordx4 (no VGPR staging): A as raw f32 through
+// a ring of KA = 6 k-tiles (5 in flight, 80 KB of HBM reads per CU), B as its
+// pre-split f16 planes through a ring of KB = 3 (L2-resident).  Each wave splits
+// its own A fragments (f32 -> scaled hi/lo f16) right before its MFMAs.
+// Swizzles are applied on the source address (the DMA destination is
+// lane-linear): A rows are 64 B, chunk c of row r sits at c ^ ((r >> 2) & 3);
+// B rows are 32 B, chunk h of row n at h ^ ((n >> 3) & 1) -- both conflict-free
+// for the 16-lane ds_read_b128 groups.  One barrier per k-tile: counted
+// vmcnt(4) retires tile t's DMA, then the barrier publishes it and frees the
+// stages of tile t - 1 for the next DMA.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ void __launch_bounds__(512, 2)
+rowgemm_g_kernel(const RowGemmArgs args) {
+  constexpr int WM = 4, WN = 2, TM = 2, TN = 4, BK = 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int KA = 6, KB = 3;
+  constexpr int A_ST = BM * BK;              // floats per A stage (16 KB)
+  constexpr int B_PL = BN * BK;              // u16 per B plane (8 KB)
+  constexpr int B_ST = 2 * B_PL;             // u16 per B stage (16 KB)
+  __shared__ __attribute__((aligned(16))) float smA[KA * A_ST];
+  __shared__ __attribute__((aligned(16))) unsigned short smB[KB * B_ST];
+  if (args.skip && *args.skip) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  int mt, ntile;
+  tile_of((args.Npad + BN - 1) / BN, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int M = args.M;
+  const int nt0 = (args.seg[0].K + BK - 1) / BK;
+  const int nt1 = args.nseg > 1 ? (args.seg[1].K + BK - 1) / BK : 0;
+  const int ntiles = nt0 + nt1;
+  const int eA0 = amax_exp(args.seg[0].amaxA);
+  const int eP0 = eA0 + amax_exp(args.seg[0].amaxB);
+  int eA1 = 0, eP1 = 0;
+  if (args.nseg > 1) {
+    eA1 = amax_exp(args.seg[1].amaxA);
+    eP1 = eA1 + amax_exp(args.seg[1].amaxB);
+  }
+  const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
+  // every ordinary global load is consumed before the first DMA: hipcc would otherwise drain
+  // the DMA ring (vmcnt(0)) at the first later use
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  if (ntiles <= 0) {
+    row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+    return;
+  }
+
+  // DMA of k-tile t (clamped into range: tail issues are dummies that keep the counts uniform)
+  auto issue = [&](int t, bool with_b) {
+    t = t < ntiles ? t : ntiles - 1;
+    const bool s1 = t >= nt0;
+    const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
+    const int k0 = (s1 ? t - nt0 : t) * BK;
+    // A: 16 rows x 64 B per wave-instruction, 2 per wave
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int blk = wave * 2 + i;
+      const int row = blk * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      int k = k0 + 4 * c;
+      k = k < sg.K - 4 ? k : sg.K - 4;
+      const float* src = sg.A + (size_t)gr * sg.lda + k;
+      glds16(src, smA + (t % KA) * A_ST + blk * 256);
+    }
+    if (with_b) {
+      // B: 32 columns x 32 B per wave-instruction, 2 per wave (planes 0/1 x 8 column blocks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int blk = wave * 2 + i;
+        const int plane = blk >> 3, sub = blk & 7;
+        const int n = sub * 32 + (lane >> 1);
+        const int h = (lane & 1) ^ ((n >> 3) & 1);
+        int gn = n0 + n;
+        gn = gn < args.Npad ? gn : args.Npad - 1;
+        const uint16_t* src = sg.B3 + (size_t)plane * sg.plane + (size_t)gn * sg.ldk + k0 + 8 * h;
+        glds16(src, smB + (t % KB) * B_ST + plane * B_PL + sub * 512);
+      }
+    }
+  };
+  auto compute = [&](int t) {
+    const float* As = smA + (t % KA) * A_ST;
+    const unsigned short* Bs = smB + (t % KB) * B_ST;
+    const float sa = t >= nt0 ? sA1 : sA0;
+    f16x8 ah[TM], al[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int r = wm * TM * 32 + tm * 32 + lr;
+      const int sw = (r >> 2) & 3;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(As + r * 16 + 4 * ((2 * lh) ^ sw));
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(As + r * 16 + 4 * ((2 * lh + 1) ^ sw));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = (j < 4 ? x0[j] : x1[j - 4]) * sa;
+        const _Float16 hh = (_Float16)x;
+        ah[tm][j] = hh;
+        al[tm][j] = (_Float16)(x - (float)hh);
+      }
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int nn = wn * TN * 32 + tn * 32 + lr;
+      const int off = nn * 16 + 8 * (lh ^ ((nn >> 3) & 1));
+      const f16x8 bh = *reinterpret_cast<const f16x8*>(Bs + off);
+      const f16x8 bl = *reinterpret_cast<const f16x8*>(Bs + B_PL + off);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        f32x16 c = acc[tm][tn];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], bh, c, 0, 0, 0);
+        acc[tm][tn] = c;
+      }
+    }
+  };
+
+  // prologue: iterations -(KA-1) .. -1 of the issue schedule (A runs KA-1 tiles ahead, B KB-1)
+#pragma unroll
+  for (int t = -(KA - 1); t < 0; ++t) {
+    issue(t + KA - 1, false);
+    if (t + KB - 1 >= 0) {
+      // B of tile t + KB - 1 (A of that tile went out earlier)
+      const int tb = t + KB - 1;
+      const int tbc = tb < ntiles ? tb : ntiles - 1;
+      const bool s1 = tbc >= nt0;
+      const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
+      const int k0 = (s1 ? tbc - nt0 : tbc) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int blk = wave * 2 + i;
+        const int plane = blk >> 3, sub = blk & 7;
+        const int n = sub * 32 + (lane >> 1);
+        const int h = (lane & 1) ^ ((n >> 3) & 1);
+        int gn = n0 + n;
+        gn = gn < args.Npad ? gn : args.Npad - 1;
+        const uint16_t* src = sg.B3 + (size_t)plane * sg.plane + (size_t)gn * sg.ldk + k0 + 8 * h;
+        glds16(src, smB + (tb % KB) * B_ST + plane * B_PL + sub * 512);
+      }
+    }
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t's B went out at iteration t - 2 and only iteration t - 1's 4 DMAs follow it
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // the stages of tile t - 1 are free now: refill them with A(t + KA - 1) and B(t + KB - 1)
+    {
+      const int ta = t + KA - 1;
+      const int tac = ta < ntiles ? ta : ntiles - 1;
+      const bool s1 = tac >= nt0;
+      const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
+      const int k0 = (s1 ? tac - nt0 : tac) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int blk = wave * 2 + i;
+        const int row = blk * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        int gr = m0 + row;
+        gr = gr < M ? gr : M - 1;
+        int k = k0 + 4 * c;
+        k = k < sg.K - 4 ? k : sg.K - 4;
+        glds16(sg.A + (size_t)gr * sg.lda + k, smA + (ta % KA) * A_ST + blk * 256);
+      }
+      const int tb = t + KB - 1;
+      const int tbc = tb < ntiles ? tb : ntiles - 1;
+      const bool sb1 = tbc >= nt0;
+      const GemmSeg& sgb = sb1 ? args.seg[1] : args.seg[0];
+      const int kb0 = (sb1 ? tbc - nt0 : tbc) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int blk = wave * 2 + i;
+        const int plane = blk >> 3, sub = blk & 7;
+        const int n = sub * 32 + (lane >> 1);
+        const int h = (lane & 1) ^ ((n >> 3) & 1);
+        int gn = n0 + n;
+        gn = gn < args.Npad ? gn : args.Npad - 1;
+        glds16(sgb.B3 + (size_t)plane * sgb.plane + (size_t)gn * sgb.ldk + kb0 + 8 * h, smB + (tb % KB) * B_ST + plane * B_PL + sub * 512);
+      }
+    }
+    if (t == nt0 && nt1 > 0) scale_acc<TM, TN>(acc, eP1 - eP0);
+    compute(t);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's dummy DMAs land before the block retires
+  scale_acc<TM, TN>(acc, -(nt1 > 0 ? eP1 : eP0));
+  row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+}
+
+template <int EPI>
+void launch_row_g(const RowGemmArgs& a, hipStream_t s) {
+  for (int i = 0; i < a.nseg; ++i)
+    if (!a.seg[i].B3 || a.seg[i].ldk < ((a.seg[i].K + 15) / 16) * 16 || a.seg[i].ldk % 8 || a.seg[i].K % 4 ||
+        a.seg[i].K < 4 || a.seg[i].lda % 4)
+      throw std::runtime_error("LDS-DMA row GEMM: bad segment");
+  const long nblk = (long)((a.M + 255) / 256) * ((a.Npad + 255) / 256);
+  hipLaunchKernelGGL((rowgemm_g_kernel<EPI>), dim3((unsigned)nblk), dim3(512), 0, s, a);
+}
+
 template <int WM, int WN, int TM, int TN, int EPI, int OCC = 2, int PF = 1>
 void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -1344,6 +1566,13 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
       case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
       case 8: launch_row3_cfg<2, 4, 2, 2, EPI, 4>(a, s); break;      // 128 x 256, 2 blocks / CU
       case 9: launch_row3_cfg<2, 4, 2, 2, EPI, 4, 2>(a, s); break;   // 128 x 256, 2 blocks / CU, 2 in flight
+      case 10:                                                        // 256 x 256, LDS-DMA ring (f16 only)
+        if (a.f16) {
+          launch_row_g<EPI>(a, s);
+          break;
+        }
+        launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
+        break;
       default: launch_row3_cfg<2, 4, 2, 2, EPI>(a, s); break;  // 128 x 256
     }
   } else {
