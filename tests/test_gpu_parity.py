@@ -280,7 +280,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_wg": 0}, {"split_wg": 1}, {"split_wg": 2}, {"split_wg": 3},
     {"split_mfma": 5, "split_wg": 1},
     {"split_mfma": 8}, {"split_mfma": 9},                     # 128 x 256, two blocks per CU
-    {"split_mfma": 10},                                       # 256 x 256, LDS-DMA ring
+    {"split_mfma": 10}, {"split_mfma": 11},                   # 256 x 256, LDS-DMA ring / BK 32
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))

@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
            sqrt(sumsq / refsq));
   };
   // modes: split tile config (0 = f32 MFMA), +100 = f16 planes
-  std::vector<int> modes = {5, 105, 110};
+  std::vector<int> modes = {105, 110, 111};
   if (argc > 3) modes = {atoi(argv[3])};   // one split mode only (profiling)
   for (int mode : modes) {
     g_options.split_mfma = mode % 100;

@@ -1525,6 +1525,143 @@ rowgemm_g_kernel(const RowGemmArgs args) {
   row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
 }
 
+// BK = 32 form of rowgemm_g_kernel (split_mfma = 11): two 32-deep k-steps per barrier, A rows of
+// 128 B (whole cache lines) and B rows of 64 B per stage, double-buffered (A 2 x 32 KB, B 2 x 32 KB).
+// Swizzles: A chunk c of row r at c ^ ((r >> 1) & 7); B chunk c of column n at c ^ ((n >> 2) & 3).
+// Needs every B plane's ldk to be a multiple of 32 (zero-filled past K).
+template <int EPI>
+__global__ void __launch_bounds__(512, 2)
+rowgemm_g32_kernel(const RowGemmArgs args) {
+  constexpr int WM = 4, WN = 2, TM = 2, TN = 4, BK = 32;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int A_ST = BM * BK;              // floats per A stage (32 KB)
+  constexpr int B_PL = BN * BK;              // u16 per B plane (16 KB)
+  constexpr int B_ST = 2 * B_PL;             // u16 per B stage (32 KB)
+  __shared__ __attribute__((aligned(16))) float smA[2 * A_ST];
+  __shared__ __attribute__((aligned(16))) unsigned short smB[2 * B_ST];
+  if (args.skip && *args.skip) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  int mt, ntile;
+  tile_of((args.Npad + BN - 1) / BN, mt, ntile);
+  const int m0 = mt * BM, n0 = ntile * BN;
+  const int M = args.M;
+  const int nt0 = (args.seg[0].K + BK - 1) / BK;
+  const int nt1 = args.nseg > 1 ? (args.seg[1].K + BK - 1) / BK : 0;
+  const int ntiles = nt0 + nt1;
+  const int eA0 = amax_exp(args.seg[0].amaxA);
+  const int eP0 = eA0 + amax_exp(args.seg[0].amaxB);
+  int eA1 = 0, eP1 = 0;
+  if (args.nseg > 1) {
+    eA1 = amax_exp(args.seg[1].amaxA);
+    eP1 = eA1 + amax_exp(args.seg[1].amaxB);
+  }
+  const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  if (ntiles <= 0) {
+    row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+    return;
+  }
+
+  auto issue = [&](int t) {
+    const bool s1 = t >= nt0;
+    const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
+    const int k0 = (s1 ? t - nt0 : t) * BK;
+    float* As = smA + (t & 1) * A_ST;
+    unsigned short* Bs = smB + (t & 1) * B_ST;
+    // A: 8 rows x 128 B per wave-instruction, 4 per wave
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int blk = wave * 4 + i;
+      const int row = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      int k = k0 + 4 * c;
+      k = k < sg.K - 4 ? k : sg.K - 4;
+      glds16(sg.A + (size_t)gr * sg.lda + k, As + blk * 256);
+    }
+    // B: 16 columns x 64 B per wave-instruction, 4 per wave (2 planes x 16 column blocks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int blk = wave * 4 + i;
+      const int plane = blk >> 4, sub = blk & 15;
+      const int n = sub * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((n >> 2) & 3);
+      int gn = n0 + n;
+      gn = gn < args.Npad ? gn : args.Npad - 1;
+      glds16(sg.B3 + (size_t)plane * sg.plane + (size_t)gn * sg.ldk + k0 + 8 * c, Bs + plane * B_PL + sub * 512);
+    }
+  };
+  auto compute = [&](int t) {
+    const float* As = smA + (t & 1) * A_ST;
+    const unsigned short* Bs = smB + (t & 1) * B_ST;
+    const float sa = t >= nt0 ? sA1 : sA0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 ah[TM], al[TM];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int r = wm * TM * 32 + tm * 32 + lr;
+        const int sw = (r >> 1) & 7;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(As + r * 32 + 4 * ((4 * ks + 2 * lh) ^ sw));
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(As + r * 32 + 4 * ((4 * ks + 2 * lh + 1) ^ sw));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = (j < 4 ? x0[j] : x1[j - 4]) * sa;
+          const _Float16 hh = (_Float16)x;
+          ah[tm][j] = hh;
+          al[tm][j] = (_Float16)(x - (float)hh);
+        }
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int nn = wn * TN * 32 + tn * 32 + lr;
+        const int off = nn * 32 + 8 * ((2 * ks + lh) ^ ((nn >> 2) & 3));
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(Bs + off);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(Bs + B_PL + off);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], bh, c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
+      }
+    }
+  };
+
+  issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                 // tile t landed (this wave's part)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ... everyone's; tile t-1 is consumed
+    if (t + 1 < ntiles) issue(t + 1);                                  // into the buffer of tile t - 1
+    if (t == nt0 && nt1 > 0) scale_acc<TM, TN>(acc, eP1 - eP0);
+    compute(t);
+  }
+  scale_acc<TM, TN>(acc, -(nt1 > 0 ? eP1 : eP0));
+  row_epilogue<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh);
+}
+
+template <int EPI>
+void launch_row_g32(const RowGemmArgs& a, hipStream_t s) {
+  for (int i = 0; i < a.nseg; ++i)
+    if (!a.seg[i].B3 || a.seg[i].ldk % 32 || a.seg[i].ldk < ((a.seg[i].K + 31) / 32) * 32 || a.seg[i].K % 4 ||
+        a.seg[i].K < 4 || a.seg[i].lda % 4)
+      throw std::runtime_error("LDS-DMA row GEMM (BK 32): bad segment");
+  const long nblk = (long)((a.M + 255) / 256) * ((a.Npad + 255) / 256);
+  hipLaunchKernelGGL((rowgemm_g32_kernel<EPI>), dim3((unsigned)nblk), dim3(512), 0, s, a);
+}
+
 template <int EPI>
 void launch_row_g(const RowGemmArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nseg; ++i)
@@ -1566,6 +1703,16 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
       case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
       case 8: launch_row3_cfg<2, 4, 2, 2, EPI, 4>(a, s); break;      // 128 x 256, 2 blocks / CU
       case 9: launch_row3_cfg<2, 4, 2, 2, EPI, 4, 2>(a, s); break;   // 128 x 256, 2 blocks / CU, 2 in flight
+      case 11: {                                                      // 256 x 256, LDS-DMA, BK 32 (f16 only)
+        bool ok = a.f16 != 0;
+        for (int i = 0; i < a.nseg; ++i) ok = ok && a.seg[i].ldk % 32 == 0;
+        if (ok) {
+          launch_row_g32<EPI>(a, s);
+          break;
+        }
+        launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
+        break;
+      }
       case 10:                                                        // 256 x 256, LDS-DMA ring (f16 only)
         if (a.f16) {
           launch_row_g<EPI>(a, s);
