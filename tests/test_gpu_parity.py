@@ -283,6 +283,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_mfma": 10}, {"split_mfma": 11},                   # 256 x 256, LDS-DMA ring / BK 32
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
+    {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -290,7 +291,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain", "split_f16")}
+                                           "split_wg", "chain", "split_f16", "split_min_k")}
     try:
         for k, v in opts.items():
             set_option(k, v)

@@ -1821,6 +1821,7 @@ static int* option_slot(const std::string& k) {
   if (k == "split_wg") return &g_options.split_wg;
   if (k == "chain") return &g_options.chain;
   if (k == "split_f16") return &g_options.split_f16;
+  if (k == "split_min_k") return &g_options.split_min_k;
   throw ArgError("unknown option " + k);
 }
 

@@ -37,7 +37,8 @@ static int env_int(const char* name, int dflt) {
 }
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
-                     env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1)};
+                     env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
+                     env_int("TRPO_SPLIT_MIN_K", 0)};
 
 namespace {
 
@@ -1687,13 +1688,23 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
                        s, a);
 }
 
+// A row GEMM whose k-loop is a few MFMA steps (the R-backward out of the softmax head: K = 2 x actions)
+// is bound by its epilogue's HBM streams; the 256 x 256 split tile holds 256 VGPRs (one block per
+// CU, nothing to overlap the epilogue with), the 128 x 256 f32 tile runs two blocks per CU.
+bool small_k_row(const RowGemmArgs& a) {
+  if (g_options.split_min_k <= 0) return false;
+  for (int i = 0; i < a.nseg; ++i)
+    if (a.seg[i].K >= g_options.split_min_k) return false;
+  return true;
+}
+
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   if constexpr (epi_is_head(EPI)) {
     if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
     if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
-  } else if (rowgemm_uses_split(a.Npad, a.epi)) {
+  } else if (rowgemm_uses_split(a.Npad, a.epi) && !small_k_row(a)) {
     switch (g_options.split_mfma) {
       case 2: launch_row3_cfg<4, 2, 2, 4, EPI>(a, s); break;   // 256 x 256
       case 3: launch_row3_cfg<2, 2, 2, 2, EPI>(a, s); break;   // 128 x 128

@@ -22,6 +22,7 @@ struct Options {
   int split_wg;    // weight gradients with fan_out > 128 on the split-bf16 MFMA (tile choice 1..3)
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
   int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
+  int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the

@@ -57,13 +57,35 @@ __global__ void amax_kernel(const float* A, int64_t n, int w, int ld, unsigned* 
   amax_wave_commit(out, mx);
 }
 
-__global__ void reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* out,
-                                   const int* skip) {
+// Sum of the S split-K slabs.  A block owns 64 consecutive parameters (one 256-B row segment per
+// wave-load) and spreads the S slabs over 16 wave groups, each with 4 independent accumulators, so a
+// launch has P/64 x 1024 threads with several loads in flight each (one thread per parameter and a
+// serial S-long chain was latency-bound: 0.2 ms for 512 slabs).
+constexpr int kRsCols = 64, kRsGroups = 16;
+__global__ void __launch_bounds__(kRsCols* kRsGroups)
+reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* out, const int* skip) {
+  __shared__ float red[kRsGroups][kRsCols + 1];
   if (skip && *skip) return;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
-       p += (int64_t)gridDim.x * blockDim.x) {
+  const int c = threadIdx.x % kRsCols, g = threadIdx.x / kRsCols;
+  const int64_t p = (int64_t)blockIdx.x * kRsCols + c;
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  if (p < P) {
+    constexpr int G = kRsGroups;
+    int s = g;
+    for (; s + 3 * G < S; s += 4 * G) {
+      a0 += slab[(int64_t)s * stride + p];
+      a1 += slab[(int64_t)(s + G) * stride + p];
+      a2 += slab[(int64_t)(s + 2 * G) * stride + p];
+      a3 += slab[(int64_t)(s + 3 * G) * stride + p];
+    }
+    for (; s < S; s += G) a0 += slab[(int64_t)s * stride + p];
+  }
+  red[g][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (g == 0 && p < P) {
     float acc = 0.0f;
-    for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * stride + p];
+#pragma unroll
+    for (int i = 0; i < kRsGroups; ++i) acc += red[i][c];
     out[p] = acc;
   }
 }
@@ -377,8 +399,9 @@ void launch_pack(const PackArgs& pa, const float* src, int which, const int* ski
 
 void launch_reduce_slab(const float* slab, int S, int64_t stride, int64_t P, float* out,
                         const int* skip, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_slab_kernel, dim3(grid_for(P, 256, 2048)), dim3(256), 0, s, slab, S, stride,
-                     P, out, skip);
+  if (P <= 0) return;
+  hipLaunchKernelGGL(reduce_slab_kernel, dim3((unsigned)((P + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups), 0, s,
+                     slab, S, stride, P, out, skip);
 }
 
 void launch_dot_partials(const float* a, const float* b, int64_t n, double* partials,
