@@ -276,8 +276,12 @@ struct trpo_engine {
     int tiles_max = 1;
     for (int l = 0; l < L; ++l)
       tiles_max = std::max(tiles_max, ((w[l] + 255) / 256) * ((w[l + 1] + 255) / 256));
-    const int s_target = std::max(1, std::min(512, 1024 / tiles_max));
     slab_stride = (P + 63) / 64 * 64;
+    int s_target = std::max(1, std::min(512, 1024 / tiles_max));
+    // narrow layers (one output tile each): a 512-split launch is 1-4 waves per CU, too few to stream
+    // the activations at HBM rate; small policies take up to 2048 splits while the slabs fit 128 MB
+    if (tiles_max == 1)
+      s_target = (int)std::max<int64_t>(s_target, std::min<int64_t>(2048, (int64_t(128) << 20) / (slab_stride * 4)));
     slab = dalloc<float>((size_t)s_target * slab_stride);
     S = s_target;
     partA = dalloc<double>(kRedBlocks * 3);
