@@ -385,3 +385,76 @@ def test_two_ranks_share_gpu_host_allreduce(gpu_available):
     res = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
     assert "MRANK OK" in res.stdout
+
+
+def _graph_sequence(eng, d, n_small):
+    """A fixed sequence of updates exercising graph capture, replay and re-keying: repeated
+    updates from theta_0, consecutive updates, a cg_iters change, a batch-size change, an
+    update from rewards.  Returns every stat dict and theta after each update."""
+    from trpo_amd import UpdateParams
+    out = []
+    th0 = d["theta"]
+    adv = np.asarray(d["advant"], np.float32)
+
+    def rec(st):
+        out.append((dict(st), eng.get_flat().copy()))
+
+    for _ in range(3):                       # eager, capture, replay
+        eng.set_flat(th0)
+        rec(eng.update(UpdateParams(cg_iters=10, residual_tol=0.0)))
+    for _ in range(2):                       # consecutive updates (theta moves; replay)
+        rec(eng.update(UpdateParams(cg_iters=10, residual_tol=0.0)))
+    for _ in range(3):                       # new key: cg_iters and the default tolerance
+        eng.set_flat(th0)
+        rec(eng.update(UpdateParams(cg_iters=5)))
+    eng.set_batch(d["X"][:n_small], d["actions"][:n_small], adv[:n_small], d["old_dist"][:n_small])
+    for _ in range(3):                       # new key: rows
+        eng.set_flat(th0)
+        rec(eng.update(UpdateParams(cg_iters=10, residual_tol=0.0, max_kl=100.0)))
+    eng.set_batch(d["X"], d["actions"], adv, d["old_dist"])
+    eng.set_rewards(d["rewards"], d["starts"])
+    for _ in range(3):                       # new key: advantages inside the graph
+        eng.set_flat(th0)
+        rec(eng.update(UpdateParams(compute_advantages=True, gamma=0.95)))
+    return out
+
+
+@pytest.mark.parametrize("name,hidden", [("update_c3.npz", None), ("update_c2.npz", None),
+                                         ("update_c3.npz", [256, 160])])
+def test_graph_replay_matches_eager(gpu_available, name, hidden):
+    """The hipGraph-replayed update prefix (option `graphs`, default on) gives bit-identical
+    results to the eager launches across capture, replay and every re-keying event; the
+    [256, 160] policy runs the split-MFMA row GEMMs instead of the fused chain."""
+    from trpo_amd._lib import get_option, set_option
+    d = dict(golden(name))
+    if hidden is not None:
+        spec = O.PolicySpec(d["X"].shape[1], hidden, spec_of(d).n_actions)
+        d.update(O.synthetic_batch(spec, d["X"].shape[0], seed=5))
+    saved = get_option("graphs")
+    runs = {}
+    try:
+        for mode in (0, 1):
+            set_option("graphs", mode)
+            eng, _ = make_engine(d) if hidden is None else _make_spec_engine(d, hidden)
+            runs[mode] = _graph_sequence(eng, d, d["X"].shape[0] // 2 + 3)
+            eng.close()
+    finally:
+        set_option("graphs", saved)
+    assert len(runs[0]) == len(runs[1])
+    for i, ((s0, t0), (s1, t1)) in enumerate(zip(runs[0], runs[1])):
+        np.testing.assert_array_equal(t0, t1, err_msg=f"theta after update {i}")
+        for k in ("cg_iters", "k", "reverted", "shs", "lm", "rate", "surr_after", "kl_after", "ent_after"):
+            assert s0[k] == s1[k], (i, k, s0[k], s1[k])
+    # the re-keyed updates really ran with their own parameters
+    assert runs[1][5][0]["cg_iters"] <= 5 and runs[1][0][0]["cg_iters"] == 10
+    assert not np.array_equal(runs[1][2][1], d["theta"])
+
+
+def _make_spec_engine(d, hidden):
+    from trpo_amd import Engine
+    spec = O.PolicySpec(d["X"].shape[1], hidden, spec_of(d).n_actions)
+    n = d["X"].shape[0]
+    eng = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+    eng.set_flat(d["theta"])
+    eng.set_batch(d["X"], d["actions"], np.asarray(d["advant"], np.float32), d["old_dist"])
+    return eng, spec

@@ -486,6 +486,7 @@ struct trpo_engine {
     allocs.clear();
     for (void* ptr : roll.mem) (void)hipFree(ptr);
     roll.mem.clear();
+    drop_graph();
     if (hsc) (void)hipHostFree(hsc);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1065,9 +1066,10 @@ struct trpo_engine {
     return vary == 0.0 ? std::nan("") : 1.0 - vard / vary;
   }
 
-  void update(const trpo_update_params& prm, trpo_update_stats* st) {
-    require_batch();
-    REQUIRE(prm.cg_iters >= 0 && prm.cg_iters <= kMaxCG, "cg_iters out of range");
+  // The update's sync-free prefix: advantages .. CG .. step scaling .. the first line-search trial
+  // (trpo_inksci.py:102-153 up to the first `loss(xnew)` of utils.py:176).  Nothing in it waits on
+  // the host, so it is replayed as one captured hipGraph (update()).
+  void update_prefix(const trpo_update_params& prm) {
     if (prm.compute_advantages) {
       Scope sp(this, "advantages");
       compute_advantages(prm.gamma);
@@ -1083,22 +1085,119 @@ struct trpo_engine {
     // shs = .5 * stepdir.dot(fisher_vector_product(stepdir)) ; lm ; fullstep ; rate  (:148-151)
     fvp(stepdir, hv, nullptr);
     {
-      // max_kl goes to the scalar block before shs_finish reads it
-      HIPCHECK(hipMemcpyAsync(&sc->max_kl, &prm.max_kl, sizeof(double), hipMemcpyHostToDevice, stream));
       Scope sp(this, "step_scale");
       launch_shs_partials(hv, stepdir, g, P, sc, partA, partB, stream);
       launch_shs_finish(partA, partB, sc, stream);
       launch_fullstep(stepdir, fullstep, P, sc, stream);
       check_launch();
     }
-    // theta = linesearch(loss, thprev, fullstep, neggdotstepdir / lm)  (:153)
-    for (int k = 0; k < 10; ++k) {
+    // theta = linesearch(loss, thprev, fullstep, neggdotstepdir / lm)  (:153): trial k = 0
+    launch_ls_trial(theta_prev, fullstep, theta_trial, P, 0, sc, stream);
+    eval_losses_dev(theta_trial);
+    launch_ls_decide(sc, 0, stream);
+    check_launch();
+  }
+
+  // hipGraph of update_prefix: keyed on everything that shapes its launches (rows, the update
+  // parameters that become kernel arguments, the baseline switch, the kernel-variant options).
+  // The first update with a key runs eagerly (lazy allocations happen there), the second captures
+  // and replays, later ones replay.  Host flags the prefix leaves behind are restored after a replay.
+  struct GraphKey {
+    int64_t n, n_global;
+    int cg_iters, adv, baseline;
+    float tol, damping;
+    double gamma;
+    Options opt;
+  };
+  GraphKey graph_key(const trpo_update_params& prm) const {
+    GraphKey k;
+    std::memset(&k, 0, sizeof k);
+    k.n = n;
+    k.n_global = n_global;
+    k.cg_iters = prm.cg_iters;
+    k.adv = prm.compute_advantages != 0;
+    k.baseline = have_baseline;
+    k.tol = prm.residual_tol;
+    k.damping = prm.cg_damping;
+    k.gamma = prm.compute_advantages ? prm.gamma : 0.0;
+    k.opt = g_options;
+    return k;
+  }
+  hipGraphExec_t upd_exec = nullptr;
+  GraphKey upd_key{};
+  bool upd_key_seen = false, graphs_broken = false;
+  struct PrefixFlags {
+    bool prepared, w3_valid, chain_w_valid, have_returns;
+  } upd_flags{};
+  void drop_graph() {
+    if (upd_exec) (void)hipGraphExecDestroy(upd_exec);
+    upd_exec = nullptr;
+    upd_key_seen = false;
+  }
+  void run_prefix(const trpo_update_params& prm) {
+    const bool graphable = g_options.graphs != 0 && !prof && world <= 1 && !graphs_broken;
+    if (!graphable) {
+      update_prefix(prm);
+      return;
+    }
+    const GraphKey key = graph_key(prm);
+    const bool same = upd_key_seen && std::memcmp(&key, &upd_key, sizeof key) == 0;
+    if (same && upd_exec) {
+      HIPCHECK(hipGraphLaunch(upd_exec, stream));
+      prepared = upd_flags.prepared;
+      w3_valid = upd_flags.w3_valid;
+      chain_w_valid = upd_flags.chain_w_valid;
+      have_returns = upd_flags.have_returns;
+      return;
+    }
+    if (!same) {
+      drop_graph();
+      update_prefix(prm);
+      upd_key = key;
+      upd_key_seen = true;
+      return;
+    }
+    // capture (the cache is rebuilt inside the graph, so the prefix must not skip prepare())
+    prepared = false;
+    hipGraph_t graph = nullptr;
+    HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+      update_prefix(prm);
+    } catch (...) {
+      (void)hipStreamEndCapture(stream, &graph);
+      if (graph) (void)hipGraphDestroy(graph);
+      graphs_broken = true;
+      throw;
+    }
+    HIPCHECK(hipStreamEndCapture(stream, &graph));
+    const hipError_t ie = hipGraphInstantiate(&upd_exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) {
+      upd_exec = nullptr;
+      graphs_broken = true;
+      (void)hipGetLastError();
+      prepared = false;
+      update_prefix(prm);
+      return;
+    }
+    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns};
+    HIPCHECK(hipGraphLaunch(upd_exec, stream));
+  }
+
+  void update(const trpo_update_params& prm, trpo_update_stats* st) {
+    require_batch();
+    REQUIRE(prm.cg_iters >= 0 && prm.cg_iters <= kMaxCG, "cg_iters out of range");
+    REQUIRE(!prm.compute_advantages || have_rewards, "no rewards: call trpo_set_rewards first");
+    // max_kl goes to the scalar block before shs_finish reads it (no prefix kernel writes it)
+    HIPCHECK(hipMemcpyAsync(&sc->max_kl, &prm.max_kl, sizeof(double), hipMemcpyHostToDevice, stream));
+    run_prefix(prm);
+    fetch_scalars();
+    for (int k = 1; k < 10 && !hsc->accepted; ++k) {
       launch_ls_trial(theta_prev, fullstep, theta_trial, P, k, sc, stream);
       eval_losses_dev(theta_trial);
       launch_ls_decide(sc, k, stream);
       check_launch();
       fetch_scalars();
-      if (hsc->accepted) break;
     }
     // sff(theta) ; losses ; revert if kl > 2 max_kl  (:154-158)
     launch_ls_finalize(theta_prev, fullstep, theta, theta_ls, P, sc, stream);
@@ -1826,6 +1925,7 @@ static int* option_slot(const std::string& k) {
   if (k == "chain") return &g_options.chain;
   if (k == "split_f16") return &g_options.split_f16;
   if (k == "split_min_k") return &g_options.split_min_k;
+  if (k == "graphs") return &g_options.graphs;
   throw ArgError("unknown option " + k);
 }
 

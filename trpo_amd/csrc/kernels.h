@@ -23,6 +23,7 @@ struct Options {
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
   int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
+  int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph (single rank)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
