@@ -171,7 +171,10 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * "narrow_pf" (prefetch depth of the narrow tiles, 1..2), "split_mfma" (0 = f32 MFMA row GEMMs;
  * 1..7 = split-bf16 row-GEMM tile for outputs wider than 128), "split_wg" (0 = f32 weight
  * gradients; 1..3 = split-bf16 tile for fan_out > 128), "fused_head" and "head_bwd"
- * (last-layer fusions; read when an engine is created).  Process-wide. */
+ * (last-layer fusions; read when an engine is created), "chain" (fused FVP chain: 0 off, 1 auto),
+ * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
+ * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph on a
+ * single-rank engine; results are bit-identical to eager launches).  Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);
 
