@@ -29,7 +29,7 @@ static float* dalloc(size_t n, unsigned seed = 0, float scale = 1.0f) {
 int main(int argc, char** argv) {
   const long M = argc > 1 ? atol(argv[1]) : 8000000;
   const int reps = argc > 2 ? atoi(argv[2]) : 5;
-  const int K = 256, N = 256;
+  const int K = getenv("GB_K") ? atoi(getenv("GB_K")) : 256, N = 256;   // GB_K: per-segment depth (main-loop length)
   float *RH = dalloc((size_t)M * K, 11), *H = dalloc((size_t)M * K, 12), *Hz = dalloc((size_t)M * N);
   float *out = dalloc((size_t)M * N), *E = dalloc((size_t)M * N, 13), *RH2 = dalloc((size_t)M * N, 14);
   float *W = dalloc(2 * K * N, 15, 0.0625f), *bias = dalloc(N);
