@@ -458,3 +458,32 @@ def _make_spec_engine(d, hidden):
     eng.set_flat(d["theta"])
     eng.set_batch(d["X"], d["actions"], np.asarray(d["advant"], np.float32), d["old_dist"])
     return eng, spec
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [(128, [256, 256], 18, 3000), (376, [1024, 1024], 17, 1200)],
+                         ids=["c4_dims", "c5_dims"])
+def test_update_bench_dims_vs_oracle(gpu_available, obs, hidden, A, n):
+    """The benchmark configurations' layer shapes (BASELINE.json configs[3] and configs[4]: split-f16 row
+    GEMMs and weight gradients, 1024-wide tiles) at a row count the float64 oracle runs in seconds:
+    undamped FVP, policy gradient, CG step direction (residual_tol = 0) and the updated parameters."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import VEC_G, VEC_STEPDIR
+    spec = O.PolicySpec(obs, hidden, A)
+    d = O.synthetic_batch(spec, n, seed=11)
+    eng = Engine(obs, hidden, A, max_rows=n)
+    eng.set_flat(d["theta"])
+    eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+    v = np.random.RandomState(12).standard_normal(spec.n_params).astype(np.float32)
+    hv = eng.fvp(v, 0.0)
+    ref = O.fvp_undamped(d["theta"].astype(np.float64), d["X"], v.astype(np.float64), spec)
+    assert_vec_close(hv, ref, REL, "Hv")
+    st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+    r = O.trpo_update(d["theta"].astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], d["old_dist"]),
+                      spec, np.float64, 10, 0.0)
+    assert_vec_close(eng.get_vector(VEC_G), r.g, REL, "g")
+    assert st["cg_iters"] == 10 == r.cg_iters
+    assert st["k"] == r.k
+    assert_vec_close(eng.get_vector(VEC_STEPDIR), r.stepdir, REL, "stepdir")
+    assert st["shs"] == pytest.approx(r.shs, rel=REL)
+    assert_vec_close(eng.get_flat(), r.theta_new, REL, "theta_new")
+    eng.close()
