@@ -75,3 +75,20 @@ def test_option_roundtrip():
         set_option("split_mfma", old)
     with pytest.raises(EngineError, match="unknown option"):
         set_option("no_such_option", 1)
+
+
+def test_every_documented_option_is_known():
+    """Every switch the header documents answers get_option; the defaults are the measured best
+    configuration: f16 split on, 256x256 two-stage split tile, chain auto, graphs on."""
+    import re
+    from trpo_amd._lib import get_option
+    text = open(os.path.join(ROOT, "include", "trpo_engine.h")).read()
+    block = text[text.index("kernel-variant switches"):text.index("int trpo_set_option")]
+    names = set(re.findall(r'"([a-z_0-9]+)"', block))
+    assert {"split_mfma", "split_f16", "chain", "graphs", "split_min_k"} <= names
+    for n in names:
+        get_option(n)
+    assert get_option("split_f16") == 1
+    assert get_option("split_mfma") == 5
+    assert get_option("chain") == 1
+    assert get_option("graphs") == 1
