@@ -69,7 +69,7 @@ CONFIGS = {
                name="C2: 50k states, obs 11, 64x64 tanh MLP, 3 actions"),
     "c3": dict(n=1_000_000, obs=128, hidden=[64, 64], A=18, cpu_rows=100_000,
                name="C3: 1M states, obs 128, 64x64 tanh MLP, 18 actions"),
-    "c4": dict(n=8_000_000, obs=128, hidden=[256, 256], A=18, cpu_rows=60_000,
+    "c4": dict(n=8_000_000, obs=128, hidden=[256, 256], A=18, cpu_rows=150_000,
                name="C4: 8M states, obs 128, 256x256 tanh MLP, 18 actions"),
     "c5": dict(n=4_000_000, obs=376, hidden=[1024, 1024], A=17, cpu_rows=4_000,
                name="C5: 4M states, obs 376, 1024x1024 tanh MLP, 17 actions"),
