@@ -255,6 +255,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # ranks beyond the visible GPUs share them (a rehearsal on a 1-GPU box); on a full node this is local_rank
+    local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -269,7 +271,13 @@ def main():
     n = hi - lo
 
     eng = Engine(cfg["obs"], cfg["hidden"], cfg["A"], max_rows=max(n, 16), device=local_rank)
-    init_engine_comm(eng, rank, world)
+    if world > torch.cuda.device_count():
+        # ranks share a GPU (rehearsal only; RCCL refuses duplicate devices): all-reduce through gloo on the host
+        def host_allreduce(arr):
+            dist.all_reduce(torch.from_numpy(arr))
+        eng.comm_set_host_allreduce(host_allreduce, rank, world)
+    else:
+        init_engine_comm(eng, rank, world)
 
     # ---- synthetic inputs, generated on the device ----
     theta0 = synthetic_theta(widths, np.random.RandomState(0))
@@ -377,7 +385,10 @@ def main():
                                                  "line search+final losses",
                        "n_states": N, "obs_dim": cfg["obs"], "hidden": cfg["hidden"], "n_actions": cfg["A"],
                        "num_params": eng.num_params, "cg_iters": 10, "residual_tol": 0.0,
-                       "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"},
+                       "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"
+                       if world <= torch.cuda.device_count() else
+                       f"dp{world} on {torch.cuda.device_count()} GPU(s): rehearsal, ranks share GPUs, "
+                       "gloo host all-reduce (not a measurement)"},
             "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak,
                          "traffic": tr[1]["traffic_bytes"] if tr else None,
