@@ -17,23 +17,27 @@ Default workload (N=1 and the scaling runs): C4 = 8,000,000 states, obs 128,
 256x256 tanh MLP, 18 actions (BASELINE.json configs[3]); with N ranks the 8M
 states are split row-wise (path-aligned), so ``scaling`` is "strong".
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel (largest
-share of HIP-event time over the timed region, on the engine's stream) against
-the roof that bounds it: its algorithmic FLOPs at the ceiling of its MFMA path
--- the f32 MFMA peak (157.3 TF/s), or for the split GEMMs (fp32 operands scaled
-and split into f16 hi+lo pieces, 3 MFMA products per fp32 product) the f16 dense
-peak / 3 = 833.3 TF/s of fp32 work (bf16 hi+mid+lo, 6 products: / 6) -- versus
-its algorithmic HBM bytes (every operand read once, every output written once)
-at 8 TB/s; the larger time is the bound ("mfma" or "hbm"), and `achieved` /
-`peak` are in that roof's unit.
-``traffic`` is the HBM bytes per launch of that kernel measured by rocprofv3
-FETCH_SIZE / WRITE_SIZE passes of this same command (tools/prof.sh ->
-tools/pmc_traffic.py -> profiles/<round>/traffic.json), when a committed file
-matches the workload.
-``cpu_baseline`` (N=1, rank 0 only) times the TF-faithful float32 CPU mirror of
-the reference (oracle/tf_graph_torch.py: every FVP recomputes forward + both
-backward passes, as each session.run does) on a bounded row sample and
-extrapolates linearly in N (every op of the update is O(N)).
+Rank 0 prints ONE JSON line.  The timed region is K updates on the production path: the
+update's sync-free prefix replayed from its captured hipGraph.  Per-kernel times come from a
+separate eager pass with per-launch HIP events on the engine's stream (events disable the
+replay; the kernels are the same launches).
+
+``roofline`` prices the dominant kernel (largest share of that event time) the way SURVEY.md
+§8(d) defines the work: ``achieved`` = its share of the FVP's algorithmic FLOPs (4ab per state
+and layer for each of R-forward, R-backward and the weight R-gradient; 2ab for layer 1's
+R-forward and weight gradient) / its average launch time, against the dense peak of the
+arithmetic it actually issues -- the f16 MFMA peak / 3 for the scaled f16 hi+lo split
+(833.3 TF/s of fp32 work), / 6 for the exact bf16 hi+mid+lo split (416.7), or the f32 MFMA
+peak (157.3).  The bytes the kernel itself streams (its materialised operands) are reported
+beside it (``own_traffic_*``), and ``traffic`` is the HBM bytes per launch measured by
+rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this command (tools/prof.sh ->
+tools/pmc_traffic.py -> profiles/<round>/traffic.json) when a committed file matches.
+``fvp.traffic_vs_algorithmic`` = bytes the FVP's kernels move / §8(d)'s N*obs*4 + 3P*4.
+``alt_arithmetic`` re-times the same workload with the exact bf16x6 split.
+``cpu_baseline`` (N=1, rank 0 only) times the TF-faithful float32 CPU mirror of the reference
+(oracle/tf_graph_torch.py: every FVP recomputes forward + both backward passes, as each
+session.run does) on a bounded row sample with every core the process may use (``host``
+reports nproc, the affinity mask and any cgroup quota) and extrapolates linearly in N.
 """
 from __future__ import annotations
 
@@ -130,6 +134,8 @@ def tag_is_split(tag: str, widths) -> bool:
 
 
 def tag_peak(tag: str, widths) -> float:
+    if tag == "fvp_chain":            # chain.hip always runs the exact bf16 hi+mid+lo split (6 products)
+        return PEAK_BF16_TFLOPS / 6
     return peak_split_tflops() if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
 
 
@@ -205,7 +211,28 @@ def synthetic_theta(widths, rng) -> np.ndarray:
     return np.concatenate(parts).astype(np.float32)
 
 
-def cpu_baseline(cfg, rows: int, threads: int):
+def host_cores():
+    """(threads to use, report): every core this process may run on, capped by a cgroup CPU quota
+    when one is set (the GPU box allots a CPU share per GPU; nproc shows the whole machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:   # pragma: no cover
+        aff = nproc
+    quota = None
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(f).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    threads = min(aff, quota) if quota else aff
+    return threads, {"nproc": nproc, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                     "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(cfg, rows: int, threads: int, core_report: dict):
     """TF-faithful float32 CPU update on `rows` states; returns a cpu_baseline dict."""
     import torch
     from oracle import trpo_oracle as O
@@ -225,8 +252,103 @@ def cpu_baseline(cfg, rows: int, threads: int):
     dt = time.perf_counter() - t0
     per_update_full = dt * cfg["n"] / rows
     return {"value": 1.0 / per_update_full, "unit": "updates/s", "cores": threads, "kind": "port",
+            "host": core_report,
             "sample": f"one full update (10 CG iters, residual_tol=0) on {rows:,} of the {cfg['n']:,} states "
-                      f"({dt:.2f} s), TF-faithful torch-CPU fp32 mirror, extrapolated linearly in N"}
+                      f"({dt:.2f} s on {threads} threads), TF-faithful torch-CPU fp32 mirror, extrapolated "
+                      f"linearly in N"}
+
+
+class Workload:
+    """The synthetic C-config batch of one rank, resident in HBM."""
+
+    def __init__(self, cfg, rank, world, local_rank, dev):
+        import torch
+        from trpo_amd.dist import shard_bounds
+        self.cfg = cfg
+        N = cfg["n"]
+        self.widths = [cfg["obs"], *cfg["hidden"], cfg["A"]]
+        # episodes every EPISODE_LEN rows -> shard cuts on path starts
+        starts = (np.arange(N) % EPISODE_LEN == 0) if N <= 50_000_000 else None
+        self.lo, self.hi = shard_bounds(N, world, starts)[rank]
+        self.n = self.hi - self.lo
+        self.rank, self.world, self.local_rank, self.dev = rank, world, local_rank, dev
+        self.theta0 = synthetic_theta(self.widths, np.random.RandomState(0))
+        self.theta0_dev = torch.from_numpy(self.theta0).to(dev)
+
+    def engine(self, comm_setup):
+        """A fresh engine holding this rank's batch (steady state: pi_old = p(theta_0))."""
+        import torch
+        from trpo_amd import Engine
+        cfg, n, dev = self.cfg, self.n, self.dev
+        eng = Engine(cfg["obs"], cfg["hidden"], cfg["A"], max_rows=max(n, 16), device=self.local_rank)
+        comm_setup(eng)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + self.rank)
+        X = torch.randn((n, cfg["obs"]), generator=g, device=dev, dtype=torch.float32)
+        actions = torch.randint(0, cfg["A"], (n,), generator=g, device=dev, dtype=torch.int64)
+        rewards = torch.rand((n,), generator=g, device=dev, dtype=torch.float64)
+        starts = ((torch.arange(self.lo, self.hi, device=dev) % EPISODE_LEN) == 0).to(torch.uint8)
+        uniform = torch.full((n, cfg["A"]), 1.0 / cfg["A"], device=dev, dtype=torch.float32)
+        zeros = torch.zeros((n,), device=dev, dtype=torch.float32)
+        eng.set_flat(self.theta0)
+        eng.set_batch(X, actions, zeros, uniform, n_global=cfg["n"])
+        old = torch.empty((n, cfg["A"]), device=dev, dtype=torch.float32)
+        eng.action_dist(out=old)                       # steady state: pi_old = p(theta_0)
+        eng.set_batch(X, actions, zeros, old, n_global=cfg["n"])
+        eng.set_rewards(rewards, starts)
+        del uniform, X, old
+        torch.cuda.synchronize()
+        return eng
+
+
+PARAMS = dict(cg_iters=10, residual_tol=0.0, cg_damping=0.1, max_kl=0.01, compute_advantages=True, gamma=0.95)
+
+
+def timed_updates(eng, wl, steps, warmup, barrier):
+    """W warmup + K timed updates (graph replay on: the production path), each from theta_0.
+    Returns (seconds, last stats)."""
+    import torch
+    from trpo_amd import UpdateParams
+    params = UpdateParams(**PARAMS)
+    last = {}
+
+    def step():
+        eng.set_flat(wl.theta0_dev)
+        last.update(eng.update(params))
+
+    for _ in range(warmup):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0, dict(last)
+
+
+def profile_pass(eng, wl, steps):
+    """Per-kernel HIP events on the engine stream over `steps` eager updates (events disable the
+    graph replay, so this pass is separate from the timed one; kernel bodies are identical)."""
+    from trpo_amd import UpdateParams
+    params = UpdateParams(**PARAMS)
+    eng.profile_reset()
+    eng.profile_enable(True)
+    for _ in range(steps):
+        eng.set_flat(wl.theta0_dev)
+        eng.update(params)
+    eng.synchronize()
+    prof = eng.profile_query()
+    eng.profile_enable(False)
+    return prof
+
+
+def fvp_tags_per_call(prof):
+    calls = prof.get("fvp_wgrad_l0", [0, 0])[0]
+    return {t: v for t, v in prof.items() if t.startswith("fvp_") or t == "split_v"}, calls
 
 
 def main():
@@ -238,15 +360,21 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="override total states (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=1, help="eager updates of the HIP-event profile pass")
+    ap.add_argument("--no-alt", action="store_true", help="skip the exact bf16x6-split comparison line")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks per node than GPUs (they share GPUs through a host all-reduce)")
     ap.add_argument("--profile-out", default="", help="write the per-tag HIP-event profile here (JSON)")
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
     if args.rows:
         cfg["n"] = args.rows
+        cfg["name"] = cfg["name"].split(":")[0] + f" dims at {args.rows:,} states (--rows override)"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
@@ -255,115 +383,101 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    # ranks beyond the visible GPUs share them (a rehearsal on a 1-GPU box); on a full node this is local_rank
-    local_rank %= max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    # one rank per GPU; ranks of this node beyond its GPUs only in an explicit rehearsal
+    rehearsal = args.rehearsal
+    if local_world > ndev and not rehearsal:
+        raise SystemExit(f"{local_world} ranks on this node but {ndev} GPU(s): pass --rehearsal to share GPUs")
+    if local_rank >= ndev and not rehearsal:
+        raise SystemExit(f"LOCAL_RANK {local_rank} has no GPU ({ndev} visible)")
+    gpu = local_rank % max(1, ndev)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
-    from trpo_amd import Engine, UpdateParams
-    from trpo_amd.dist import init_engine_comm, shard_bounds
+    from trpo_amd.dist import init_engine_comm
 
-    N = cfg["n"]
-    widths = [cfg["obs"], *cfg["hidden"], cfg["A"]]
-    starts_all = None   # episodes every EPISODE_LEN rows -> shard cuts on path starts
-    bounds = shard_bounds(N, world, (np.arange(N) % EPISODE_LEN == 0) if N <= 50_000_000 else starts_all)
-    lo, hi = bounds[rank]
-    n = hi - lo
-
-    eng = Engine(cfg["obs"], cfg["hidden"], cfg["A"], max_rows=max(n, 16), device=local_rank)
-    if world > torch.cuda.device_count():
-        # ranks share a GPU (rehearsal only; RCCL refuses duplicate devices): all-reduce through gloo on the host
-        def host_allreduce(arr):
-            dist.all_reduce(torch.from_numpy(arr))
-        eng.comm_set_host_allreduce(host_allreduce, rank, world)
-    else:
-        init_engine_comm(eng, rank, world)
-
-    # ---- synthetic inputs, generated on the device ----
-    theta0 = synthetic_theta(widths, np.random.RandomState(0))
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    X = torch.randn((n, cfg["obs"]), generator=g, device=dev, dtype=torch.float32)
-    actions = torch.randint(0, cfg["A"], (n,), generator=g, device=dev, dtype=torch.int64)
-    rewards = torch.rand((n,), generator=g, device=dev, dtype=torch.float64)
-    starts = ((torch.arange(lo, hi, device=dev) % EPISODE_LEN) == 0).to(torch.uint8)
-    uniform = torch.full((n, cfg["A"]), 1.0 / cfg["A"], device=dev, dtype=torch.float32)
-    zeros = torch.zeros((n,), device=dev, dtype=torch.float32)
-    eng.set_flat(theta0)
-    eng.set_batch(X, actions, zeros, uniform, n_global=N)
-    old = torch.empty((n, cfg["A"]), device=dev, dtype=torch.float32)
-    eng.action_dist(out=old)                       # steady state: pi_old = p(theta_0)
-    eng.set_batch(X, actions, zeros, old, n_global=N)
-    eng.set_rewards(rewards, starts)
-    del uniform, X
-    theta0_dev = torch.from_numpy(theta0).to(dev)
-    params = UpdateParams(cg_iters=10, residual_tol=0.0, cg_damping=0.1, max_kl=0.01,
-                          compute_advantages=True, gamma=0.95)
-
-    last = {}
-
-    def step():
-        eng.set_flat(theta0_dev)
-        last.update(eng.update(params))
-
-    for _ in range(args.warmup):
-        step()
+    def comm_setup(eng):
+        if world <= 1:
+            return
+        if rehearsal:
+            # ranks share a GPU (RCCL refuses duplicate devices): all-reduce through gloo on the host
+            def host_allreduce(arr):
+                dist.all_reduce(torch.from_numpy(arr))
+            eng.comm_set_host_allreduce(host_allreduce, rank, world)
+        else:
+            init_engine_comm(eng, rank, world)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    eng.synchronize()
-    torch.cuda.synchronize()
-    barrier()
-    eng.profile_reset()
-    eng.profile_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    eng.synchronize()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = eng.profile_query()
-    eng.profile_enable(False)
+    wl = Workload(cfg, rank, world, gpu, dev)
+    n, widths, N = wl.n, wl.widths, cfg["n"]
+    eng = wl.engine(comm_setup)
+    elapsed, last = timed_updates(eng, wl, args.steps, args.warmup, barrier)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    prof = profile_pass(eng, wl, max(1, args.profile_steps))
+    num_params = eng.num_params
+    prod = split_products()
+    eng.close()
+    del eng
+    torch.cuda.empty_cache()
+
+    alt = None
+    if not args.no_alt and world == 1:
+        # the exact bf16 hi+mid+lo split (6 products) on the same workload, beside the default
+        from trpo_amd._lib import get_option, set_option
+        saved = get_option("split_f16")
+        set_option("split_f16", 0)
+        try:
+            e2 = wl.engine(comm_setup)
+            t2, _ = timed_updates(e2, wl, max(1, min(args.steps, 3)), 1, barrier)
+            e2.close()
+            del e2
+            torch.cuda.empty_cache()
+        finally:
+            set_option("split_f16", saved)
+        k2 = max(1, min(args.steps, 3))
+        alt = {"arithmetic": "bf16x6: every fp32 operand split exactly into hi+mid+lo bf16 (6 products)",
+               "value": k2 / t2, "unit": "updates/s", "ms_per_step": 1e3 * t2 / k2, "steps": k2}
 
     if args.profile_out and rank == 0:
         with open(args.profile_out, "w") as f:
-            json.dump({"profile": prof, "steps": args.steps, "n_local": n, "widths": widths}, f, indent=1)
+            json.dump({"profile": prof, "profile_steps": args.profile_steps, "n_local": n, "widths": widths}, f,
+                      indent=1)
 
     if rank == 0:
-        # ---- roofline of the dominant kernel (HIP events on the engine stream) ----
+        # ---- roofline of the dominant kernel (HIP events on the engine stream, profile pass) ----
+        psteps = max(1, args.profile_steps)
         kernel_tags = {t: v for t, v in prof.items() if tag_flops(t, widths, n) > 0}
         dom = max(kernel_tags, key=lambda t: kernel_tags[t][1])
         cnt, tot_ms = kernel_tags[dom]
         avg_s = tot_ms / cnt / 1e3
         fl = tag_flops(dom, widths, n)
         by = tag_bytes(dom, widths, n)
-        bound, _ = tag_roof(dom, widths, n)
-        if bound == "hbm":
-            achieved, peak, unit = by / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
-            peak_basis = "HBM3E 8.0 TB/s"
-        else:
-            achieved, peak, unit = fl / avg_s / 1e12, tag_peak(dom, widths), "TFLOP/s"
-            peak_basis = ("split MFMA: f16/bf16 dense peak / %d products" % split_products()
-                          if tag_is_split(dom, widths) else "f32 MFMA peak")
-        upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / args.steps
-        # seconds one update would take with every kernel at its own roof (max of MFMA and HBM time)
-        upd_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / args.steps
+        peak = tag_peak(dom, widths)
+        achieved = fl / avg_s / 1e12
+        peak_basis = (f"split MFMA: f16/bf16 dense peak 2.5 PF / {prod} products" if tag_is_split(dom, widths)
+                      else "f32 MFMA peak")
+        upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / psteps
+        upd_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / psteps
         tr = committed_traffic(args.config, N, dom) if world == 1 else None
         upd_s = elapsed / args.steps
-        fvp_ms = sum(ms for t, (c, ms) in prof.items() if t.startswith("fvp_") or t == "reduce")
-        fvp_calls = prof.get("fvp_wgrad_l0", [0, 0])[0]
+        fvp_tags, fvp_calls = fvp_tags_per_call(prof)
+        fvp_ms = sum(ms for _, (_, ms) in fvp_tags.items()) + prof.get("reduce", [0, 0])[1] * (
+            fvp_calls / max(1, prof.get("reduce", [1, 1])[0]))
         fvp_s = fvp_ms / max(1, fvp_calls) / 1e3 if fvp_calls else float("nan")
-        fvp_bytes = n * cfg["obs"] * 4 + 3 * eng.num_params * 4
+        fvp_alg_bytes = n * cfg["obs"] * 4 + 3 * num_params * 4
+        fvp_moved = sum(tag_bytes(t, widths, n) * c for t, (c, _) in fvp_tags.items()) / max(1, fvp_calls)
+        arith = ("f16x3" if prod == 3 else "bf16x6")
+        value = args.steps / elapsed
+        metric = METRIC
         out = {
-            "metric": METRIC,
-            "value": args.steps / elapsed,
+            "metric": metric,
+            "value": value,
             "unit": "updates/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -372,49 +486,63 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": f"fp32 ({arith} split)",
             "arithmetic": ("fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on f16 MFMA with each "
                            "fp32 operand scaled by a power of two and split into hi+lo f16 pieces (3 products, "
-                           "error 2^-22 relative)" if split_products() == 3 else
+                           "error 2^-22 relative)" if prod == 3 else
                            "fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on bf16 MFMA with "
                            "each fp32 operand split exactly into hi+mid+lo bf16 pieces (6 products)") +
                           "; narrower GEMMs on f32 MFMA; softmax heads and CG scalars in f64",
             "data": "synthetic (X~N(0,1), a~U{0..A-1}, rewards~U(0,1), paths of 200 steps, "
                     "random-init policy, pi_old = p(theta_0))",
+            "timing": "timed region = K updates replayed from the captured update hipGraph (production path); "
+                      "kernel times from a separate eager pass with per-launch HIP events",
             "config": {"workload": cfg["name"] + "; full update = discount+standardise+pg+10 CG+shs FVP+"
                                                  "line search+final losses",
                        "n_states": N, "obs_dim": cfg["obs"], "hidden": cfg["hidden"], "n_actions": cfg["A"],
-                       "num_params": eng.num_params, "cg_iters": 10, "residual_tol": 0.0,
+                       "num_params": num_params, "cg_iters": 10, "residual_tol": 0.0,
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"
-                       if world <= torch.cuda.device_count() else
-                       f"dp{world} on {torch.cuda.device_count()} GPU(s): rehearsal, ranks share GPUs, "
-                       "gloo host all-reduce (not a measurement)"},
-            "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak,
-                         "unit": unit, "frac": achieved / peak,
+                       if not rehearsal or world == 1 else
+                       f"dp{world} on {ndev} GPU(s): rehearsal, ranks share GPUs, gloo host all-reduce"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": tr[1]["traffic_bytes"] if tr else None,
                          "peak_basis": peak_basis,
-                         "algorithmic_bytes_per_launch": by, "flops_per_launch": fl,
-                         "mfma_tflops": fl / avg_s / 1e12, "mfma_peak": tag_peak(dom, widths),
-                         "hbm_gbs_algorithmic": by / avg_s / 1e9,
+                         "achieved_basis": "SURVEY.md §8(d) algorithmic FLOPs of this kernel's share of the FVP "
+                                           "(4ab R-forward / 4ab R-backward / 4ab weight-R-gradient per state and "
+                                           "layer) / its average launch time",
+                         "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt,
+                         "own_traffic_bytes_per_launch": by,
+                         "own_traffic_hbm_gbs": by / avg_s / 1e9,
+                         "own_traffic_hbm_frac": by / avg_s / 1e9 / PEAK_HBM_GBS,
                          "hbm_gbs_at_traffic": tr[1]["traffic_bytes"] / avg_s / 1e9 if tr else None,
-                         "traffic_source": tr[0] if tr else None,
-                         "avg_launch_ms": avg_s * 1e3, "launches": cnt},
+                         "traffic_source": tr[0] if tr else None},
             "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
                                 "achieved_tflops": upd_flops * world / upd_s / 1e12,
                                 "roof_ms_per_update": upd_peak_s * 1e3,
                                 "frac_of_roof": upd_peak_s / upd_s},
-            "fvp": {"ms_per_fvp": fvp_s * 1e3, "gbps_algorithmic": fvp_bytes / fvp_s / 1e9,
-                    "hbm_frac": fvp_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
+            "fvp": {"ms_per_fvp": fvp_s * 1e3,
+                    "gbps_algorithmic": fvp_alg_bytes / fvp_s / 1e9,
+                    "hbm_frac_algorithmic": fvp_alg_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
+                    "algorithmic_bytes": fvp_alg_bytes,
+                    "moved_bytes": fvp_moved,
+                    "traffic_vs_algorithmic": fvp_moved / fvp_alg_bytes,
                     "tflops": fvp_flops_per_row(widths) * n / fvp_s / 1e12},
+            "alt_arithmetic": alt,
             "last_update": {k: last[k] for k in ("cg_iters", "k", "reverted", "kl_after", "surr_after")},
             "cpu_baseline": None,
         }
+        if rehearsal and world > 1:
+            # ranks shared GPUs: not a measurement of N GPUs
+            out["rehearsal"] = True
+            out["n_gpus"] = min(ndev, local_world)
+            out["rehearsal_updates_per_s"] = value
+            out["value"] = None
+            out["update_roofline"]["achieved_tflops"] = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-                threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+            threads, rep = host_cores()
             rows = args.cpu_rows or min(cfg["cpu_rows"], N)
-            out["cpu_baseline"] = cpu_baseline(cfg, rows, threads)
+            out["cpu_baseline"] = cpu_baseline(cfg, rows, threads, rep)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -120,6 +120,13 @@ int trpo_set_rewards(trpo_engine* e, const double* rewards, const uint8_t* episo
 int trpo_compute_advantages(trpo_engine* e, double gamma, double* returns_out, double* advant_out,
                             int mem);
 
+/* adv = (adv - adv.mean()) / (adv.std() + 1e-8) in place, float64, population std
+ * (trpo_inksci.py:115-117; SURVEY.md §8(b) `standardize(adv, n)`).  adv32_out (may be NULL) receives
+ * float32(adv), what the advant placeholder is fed (:121).  With an engine the two sums run over all
+ * ranks of its communicator (n = this rank's rows, n_global = all ranks') on its stream; e = NULL
+ * runs on the current device for one process (n_global must equal n). */
+int trpo_standardize(trpo_engine* e, double* adv, int64_t n, int64_t n_global, float* adv32_out, int mem);
+
 /* ---- the graph outputs ---------------------------------------------------- */
 /* session.run(self.losses) -> [surr, kl, ent] at the current parameters (trpo_inksci.py:53,156) */
 int trpo_losses(trpo_engine* e, float out3[3]);
@@ -226,7 +233,7 @@ typedef struct trpo_feed_view {
   const float* old_dist;     /* [n][ld_old] f32 */
   int ld_old;
   const uint8_t* episode_starts;   /* [n] */
-  const double* returns;     /* [n] f64, valid after the advantages were computed */
+  const double* returns;     /* [n] f64 after the advantages of this feed were computed, else NULL */
   double* baseline;          /* [n] f64; trpo_set_baseline(e, view.baseline, TRPO_MEM_DEVICE) marks it set */
 } trpo_feed_view;
 int trpo_get_feed_view(trpo_engine* e, trpo_feed_view* out);

@@ -1,0 +1,119 @@
+"""The FVP at BASELINE.json's headline size: C4 layer shapes (obs 128, 256x256, 18 actions) over
+N = 8M states, where the 256-wide GEMMs run on the scaled f16 hi+lo split.
+
+At that N the KL_ff plain deltas D_l are O(eps/N) ~ 1e-13 and the power-of-two operand scales
+come from running maxima over the whole batch, a numerical regime the small-N parity tests do not
+reach (trpo_inksci.py:56-70).  The oracle cannot evaluate 8M states in test time, so the full
+batch is checked through size-independent properties of a Hessian-vector product, and the
+n_global = 8M scaling through a row slice the oracle does evaluate:
+
+* symmetry      u.Hv = v.Hu               (relative to |u||Hv|, 1e-5)
+* linearity     H(a u + b v) = a Hu + b Hv (norm-relative 1e-5)
+* curvature     v.Hv > 0 for random v (KL_ff's Hessian near its minimum)
+* shard sums    Hv(8M) = sum over 8 row shards of Hv(shard, n_global = 8M), each shard with its own
+                running-max scales (norm-relative 1e-5)
+* arithmetic    f16x3 split vs the exact bf16x6 split on the same 8M batch (norm-relative 1e-5)
+* slice         3000 rows with n_global = 8M against the float64 oracle (SURVEY.md §8(d) bar)
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_vec_close, rel_l2
+from oracle import trpo_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N = 8_000_000
+SPEC = O.PolicySpec(128, [256, 256], 18)
+REL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def big_batch():
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((N, SPEC.obs_dim), dtype=np.float32)
+    actions = rng.integers(0, SPEC.n_actions, N, dtype=np.int64)
+    theta = O.init_theta(SPEC, np.random.RandomState(1)).astype(np.float32)
+    u = np.random.RandomState(2).standard_normal(SPEC.n_params).astype(np.float32)
+    v = np.random.RandomState(3).standard_normal(SPEC.n_params).astype(np.float32)
+    return {"X": X, "actions": actions, "theta": theta, "u": u, "v": v}
+
+
+def _engine(b, rows=None, n_global=N):
+    from trpo_amd import Engine
+    lo, hi = rows or (0, N)
+    e = Engine(SPEC.obs_dim, SPEC.hidden, SPEC.n_actions, max_rows=hi - lo)
+    e.set_flat(b["theta"])
+    X, a = b["X"][lo:hi], b["actions"][lo:hi]
+    uniform = np.full((hi - lo, SPEC.n_actions), 1.0 / SPEC.n_actions, np.float32)
+    e.set_batch(X, a, None, uniform, n_global=n_global)
+    old = e.action_dist()                                  # steady state: pi_old = p(theta)
+    e.set_batch(X, a, None, old, n_global=n_global)
+    return e, old
+
+
+@pytest.fixture(scope="module")
+def hv_f16(big_batch):
+    from trpo_amd._lib import get_option
+    assert get_option("split_f16") == 1
+    e, old = _engine(big_batch)
+    u, v = big_batch["u"], big_batch["v"]
+    out = {"Hu": e.fvp(u, 0.0), "Hv": e.fvp(v, 0.0), "H(2u-3v)": e.fvp(2.0 * u - 3.0 * v, 0.0)}
+    big_batch["old"] = old
+    e.close()
+    return out
+
+
+def test_c4_8m_symmetry_and_curvature(gpu_available, big_batch, hv_f16):
+    u, v = big_batch["u"].astype(np.float64), big_batch["v"].astype(np.float64)
+    Hu, Hv = hv_f16["Hu"].astype(np.float64), hv_f16["Hv"].astype(np.float64)
+    asym = abs(u @ Hv - v @ Hu) / (np.linalg.norm(u) * np.linalg.norm(Hv))
+    assert asym < REL, asym
+    assert v @ Hv > 0 and u @ Hu > 0
+
+
+def test_c4_8m_linearity(gpu_available, hv_f16):
+    comb = 2.0 * hv_f16["Hu"].astype(np.float64) - 3.0 * hv_f16["Hv"].astype(np.float64)
+    assert_vec_close(hv_f16["H(2u-3v)"], comb, REL, "H(2u-3v) vs 2Hu-3Hv at 8M")
+
+
+def test_c4_8m_shard_sums(gpu_available, big_batch, hv_f16):
+    total = np.zeros(SPEC.n_params)
+    bounds = np.linspace(0, N, 9).astype(np.int64)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        from trpo_amd import Engine
+        e = Engine(SPEC.obs_dim, SPEC.hidden, SPEC.n_actions, max_rows=int(hi - lo))
+        e.set_flat(big_batch["theta"])
+        e.set_batch(big_batch["X"][lo:hi], big_batch["actions"][lo:hi], None, big_batch["old"][lo:hi],
+                    n_global=N)
+        total += e.fvp(big_batch["v"], 0.0).astype(np.float64)
+        e.close()
+    assert_vec_close(hv_f16["Hv"], total, REL, "Hv(8M) vs sum of 8 shard partials")
+
+
+def test_c4_8m_f16_split_vs_exact_bf16_split(gpu_available, big_batch, hv_f16):
+    from trpo_amd._lib import get_option, set_option
+    saved = get_option("split_f16")
+    set_option("split_f16", 0)
+    try:
+        e, _ = _engine(big_batch)
+        hv6 = e.fvp(big_batch["v"], 0.0)
+        e.close()
+    finally:
+        set_option("split_f16", saved)
+    r = rel_l2(hv_f16["Hv"], hv6)
+    print(f"f16x3 vs bf16x6 at 8M: rel L2 {r:.2e}")
+    assert_vec_close(hv_f16["Hv"], hv6, REL, "f16x3 vs bf16x6 Hv at 8M")
+
+
+def test_c4_slice_at_n_global_8m_vs_oracle(gpu_available, big_batch):
+    """3000 rows of the 8M batch with 1/N_global = 1/8M: D_l ~ eps/8M sets the f16 operand scales
+    near 2^55; the result must still meet the 1e-5 bar against the float64 oracle."""
+    n = 3000
+    e, old = _engine(big_batch, rows=(0, n), n_global=N)
+    v = big_batch["v"]
+    hv = e.fvp(v, 0.0)
+    e.close()
+    ref = O.fvp_undamped(big_batch["theta"].astype(np.float64), big_batch["X"][:n], v.astype(np.float64), SPEC,
+                         n_global=N)
+    assert_vec_close(hv, ref, REL, "Hv of a 3000-row slice at n_global = 8M")

@@ -3,6 +3,8 @@
 import numpy as np
 import pytest
 
+from conftest import rel_l2
+
 pytestmark = pytest.mark.gpu
 
 
@@ -56,3 +58,126 @@ def test_utils_cat_sample_and_rollout_dropins(gpu_available):
     assert sum(len(p["rewards"]) for p in paths) >= 500
     assert all(p["obs"].shape == (len(p["rewards"]), 4) and p["action_dists"].shape == (len(p["rewards"]), 2)
                for p in paths)
+
+
+# ---------------------------------------------------------------------------- learn() vs the oracle loop
+N_ITER = 3
+
+
+def _draws(seed, n_iter, n_timesteps=1000, ep_max=200):
+    """Recorded env.reset / cat_sample uniforms per iteration, as the reference's loop draws them
+    (one environment: [1][max_episodes][4] and [1][budget + ep_max - 1])."""
+    rng = np.random.RandomState(seed)
+    ru = [rng.random_sample((1, n_timesteps, 4)) for _ in range(n_iter)]
+    au = [rng.random_sample((1, n_timesteps + ep_max - 1)) for _ in range(n_iter)]
+    return lambda i: (ru[i], au[i], n_timesteps)
+
+
+def _oracle_inputs():
+    from trpo_amd.agent import xavier_theta
+    from trpo_amd.vf import vf_xavier_params
+    rng = np.random.RandomState(1)                       # Session.init_rng (utils.py:7-9 seed)
+    th0 = xavier_theta(4, [64], 2, rng)                  # TRPOAgent's initial policy
+    th1 = xavier_theta(4, [64], 2, rng)                  # tf.initialize_all_variables() at the first VF fit
+    return th0, th1, (lambda F: vf_xavier_params(F, (64, 64), np.random.RandomState(1)))
+
+
+def test_learn_matches_oracle_loop(gpu_available):
+    """Three learn() iterations (rollout -> VF predict -> advantages -> VF fit -> update ->
+    explained variance, trpo_inksci.py:88-176) on the device against the oracle loop with the same
+    recorded draws.  The oracle replays the device's sampled trajectory (its actions follow the
+    device's action_dists under the same uniforms), so per-iteration numbers compare on identical
+    paths; its own policy on those states must match the device's dists.  Bars: paths, actions,
+    starts, rewards exact; returns 1e-12; baselines / advantages 1e-4 (the float32 VF after 50 Adam
+    steps, tests/test_gpu_vf.py); k exact; surr / kl / ent / explained variance 1e-3 relative."""
+    from trpo_amd import TRPOAgent
+    from oracle import learn_oracle
+    draws = _draws(11, N_ITER)
+    agent = TRPOAgent(4, 2, hidden=(64,), max_rows=4096)
+    hist = agent.learn(max_iterations=N_ITER, n_envs=1, log=None, draws=draws, record=True)
+    th0, th1, vf_init = _oracle_inputs()
+    ref = learn_oracle.learn(th0, [4, 64, 2], N_ITER, draws, th1, vf_init,
+                             dists_from=lambda i: hist[i]["rollout"]["action_dists"])
+    assert len(hist) == len(ref) == N_ITER
+    for i, (h, r) in enumerate(zip(hist, ref)):
+        ro_d, ro_o = h["rollout"], r["rollout"]
+        assert h["steps"] == r["steps"] and h["paths"] == r["paths"], i
+        assert np.array_equal(ro_d["actions"], ro_o["actions"]), i
+        assert np.array_equal(ro_d["starts"], ro_o["starts"]) and np.array_equal(ro_d["rewards"], ro_o["rewards"])
+        assert np.allclose(ro_d["obs"], ro_o["obs"], rtol=1e-12, atol=1e-14), i
+        # the oracle's own policy on the device's states (theta after i updates)
+        tol = 1e-6 if i == 0 else 1e-4
+        assert np.max(np.abs(ro_d["action_dists"] - r["policy_dists"])) < tol, i
+        assert np.allclose(h["returns"], r["returns"], rtol=1e-12), i
+        if i == 0:
+            assert not np.any(h["baseline"]) and not np.any(r["baseline"])
+        else:
+            assert rel_l2(h["baseline"], r["baseline"]) < 1e-4, (i, rel_l2(h["baseline"], r["baseline"]))
+        assert rel_l2(h["advantages"], r["advantages"]) < 1e-4, (i, rel_l2(h["advantages"], r["advantages"]))
+        assert h["k"] == r["k"] and h["reverted"] == r["reverted"], (i, h["k"], r["k"])
+        for key in ("surr", "kl", "ent", "explained_variance"):
+            hk = "entropy" if key == "ent" else key
+            assert h[hk] == pytest.approx(r[hk], rel=1e-3, abs=1e-7), (i, key, h[hk], r[hk])
+    assert hist[0]["reverted"] == ref[0]["reverted"]
+
+
+def test_learn_argmax_phase_and_end_count_exit(gpu_available):
+    """trpo_inksci.py:137-141,174-175: once the baseline explains > 0.8 of the returns' variance,
+    training stops, the rollouts take the argmax action, and the loop ends after end_count passes
+    100.  The explained variance is forced above 0.8 at iteration 1 (control-flow test)."""
+    from trpo_amd import TRPOAgent
+    agent = TRPOAgent(4, 2, hidden=(64,), max_rows=4096)
+    real_ev = agent.engine.explained_variance
+    calls = []
+
+    def forced_ev():
+        calls.append(real_ev())
+        return 0.9 if len(calls) >= 2 else calls[-1]
+    agent.engine.explained_variance = forced_ev
+    hist = agent.learn(max_iterations=200, n_envs=1, seed=5, log=None)
+    trained = [h for h in hist if h["train"]]
+    frozen = [h for h in hist if not h["train"]]
+    assert len(trained) == 2 and len(calls) == 2
+    assert len(frozen) == 101 and frozen[-1]["end_count"] == 101
+    assert len(hist) == 103 and hist[-1]["iteration"] == 102
+    theta = agent.engine.get_flat()
+    # argmax rollouts never change the policy; two identical draws give identical paths
+    agent.engine.rollout_cartpole(n_envs=1, n_timesteps=1000, train=False, seed=2)
+    ro = agent.engine.rollout_fetch()
+    from oracle.cartpole_oracle import policy_dist32
+    assert np.array_equal(ro["actions"], np.argmax(ro["action_dists"], axis=1))
+    assert np.max(np.abs(ro["action_dists"] - policy_dist32(theta, ro["obs"], [4, 64, 2]))) < 1e-6
+    assert np.array_equal(agent.engine.get_flat(), theta)
+
+
+def test_learn_mean_reward_stop_rule(gpu_available):
+    """trpo_inksci.py:135-136: a mean episode reward above 1.1*500 stops training (unreachable on
+    CartPole-v0's 200-step limit, so the statistics the loop reads are scaled: control flow only)."""
+    from trpo_amd import TRPOAgent
+    agent = TRPOAgent(4, 2, hidden=(64,), max_rows=4096)
+    real = agent.engine.rollout_fetch_stats
+    agent.engine.rollout_fetch_stats = lambda: {k: (v * 50.0 if k == "rewards" else v) for k, v in real().items()}
+    hist = agent.learn(max_iterations=5, n_envs=1, seed=2, log=None)
+    assert all(not h["train"] for h in hist)
+    assert [h["end_count"] for h in hist] == [1, 2, 3, 4, 5]
+    assert agent.vf.net is None            # never fitted
+
+
+def test_learn_nan_entropy_exit(gpu_available):
+    """trpo_inksci.py:172-173: a NaN entropy ends the loop (the reference calls exit(-1)).  A NaN
+    policy parameter after the first update makes every loss NaN on the next one."""
+    from trpo_amd import TRPOAgent
+    agent = TRPOAgent(4, 2, hidden=(64,), max_rows=4096)
+    real_update = agent.engine.update
+    n_upd = []
+
+    def update(params):
+        n_upd.append(1)
+        if len(n_upd) == 2:
+            th = agent.engine.get_flat()
+            th[3] = np.nan
+            agent.engine.set_flat(th)
+        return real_update(params)
+    agent.engine.update = update
+    hist = agent.learn(max_iterations=10, n_envs=1, seed=3, log=None)
+    assert len(hist) == 2 and hist[-1].get("nan_exit") and np.isnan(hist[-1]["entropy"])

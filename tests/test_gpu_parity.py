@@ -365,11 +365,8 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
     assert_vec_close(out[1], out[0], REL, f"chain vs row-GEMM Hv {obs} {hidden} {A}")
 
 
-def test_two_ranks_share_gpu_host_allreduce(gpu_available):
-    """Two processes, one GPU: the engine's whole multi-rank sequence (path-aligned shards,
-    1/N_global partials, all-reduced FVP / gradient / losses / standardisation sums, replicated
-    CG) with the all-reduce carried by gloo; ranks must end bitwise identical and equal a
-    single-rank engine."""
+def run_mrank(*extra, nproc=2, timeout=600):
+    """tools/mrank_check.py under torch.distributed.run (gloo rendezvous on 127.0.0.1)."""
     import os
     import socket
     import subprocess
@@ -379,12 +376,29 @@ def test_two_ranks_share_gpu_host_allreduce(gpu_available):
     sock.bind(("127.0.0.1", 0))
     port = sock.getsockname()[1]
     sock.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tools", "mrank_check.py"),
-           "--host-allreduce"]
-    res = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
+           *extra]
+    res = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout)
     assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
     assert "MRANK OK" in res.stdout
+    print(res.stdout.strip().splitlines()[-2])
+
+
+def test_two_ranks_share_gpu_host_allreduce(gpu_available):
+    """Two processes, one GPU: the engine's whole multi-rank sequence (path-aligned shards,
+    1/N_global partials, all-reduced FVP / gradient / losses / standardisation sums, replicated
+    CG) with the all-reduce carried by gloo; ranks must end bitwise identical and equal a
+    single-rank engine; the captured update graph (host all-reduce nodes inside) replays
+    bitwise identically to the eager update."""
+    run_mrank("--host-allreduce", "--graphs")
+
+
+def test_two_ranks_c4_dims_f16_split(gpu_available):
+    """The same at C4 layer shapes (obs 128, 256x256, 18 actions), where the 256-wide GEMMs run
+    on the scaled f16 hi+lo split: the running-max operand scales are per rank, the all-reduced
+    partials must still give bitwise-identical ranks within 1e-5 of one rank (trpo_inksci.py:56-70,147)."""
+    run_mrank("--host-allreduce", "--graphs", "--dims", "c4", "--rows", "120000")
 
 
 def _graph_sequence(eng, d, n_small):

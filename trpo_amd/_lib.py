@@ -69,6 +69,7 @@ SIGNATURES = {
     "trpo_set_batch": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "trpo_set_rewards": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "trpo_compute_advantages": (c_int, [c_void_p, c_double, c_void_p, c_void_p, c_int]),
+    "trpo_standardize": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int]),
     "trpo_losses": (c_int, [c_void_p, POINTER(c_float)]),
     "trpo_eval_losses": (c_int, [c_void_p, c_void_p, POINTER(c_float), c_int]),
     "trpo_action_dist": (c_int, [c_void_p, c_void_p, c_int]),

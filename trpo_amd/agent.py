@@ -146,15 +146,26 @@ class TRPOAgent:
 
     # ------------------------------------------------------------------ trpo_inksci.py:89-177
     def learn(self, max_iterations: Optional[int] = None, n_envs: int = 1, seed: int = 1,
-              log: Optional[Callable[[str], None]] = print) -> List[dict]:
+              log: Optional[Callable[[str], None]] = print,
+              draws: Optional[Callable[[int], tuple]] = None, record: bool = False) -> List[dict]:
         """The reference's learn() loop on CartPole-v0, device-resident.  Stop rules as
         trpo_inksci.py:131-141,172-175: training stops when the mean episode reward exceeds
         1.1*500 or the baseline explains > 0.8 of the returns' variance; the loop then keeps
         rolling out the argmax policy and ends after 100 such iterations; a NaN entropy ends it
         (the reference calls exit(-1)).  max_iterations bounds the loop (None: as the reference).
+        draws(i) -> (reset_uniforms, action_uniforms, max_episodes_per_env) injects the random draws
+        of iteration i's rollout (env.reset and cat_sample; tests), else a Philox stream per iteration.
+        record=True also returns each iteration's rollout arrays, baselines, returns and
+        standardised advantages (host copies; parity tests).
         Returns one stats dict per iteration."""
         cfg = self.config
         eng = self.engine
+        # worst case rows of one rollout: every environment overshoots its budget by one episode
+        budget = -(-cfg["episodes_per_roll"] // n_envs)
+        worst = n_envs * (budget + min(cfg["max_steps"], 200) - 1)
+        if worst > eng.max_rows:
+            raise ValueError(f"learn(): a rollout of {n_envs} environments can reach {worst} steps, more than "
+                             f"max_rows={eng.max_rows}; create the agent with max_rows >= {worst}")
         say = log or (lambda _s: None)
         start_time = time.time()
         i = 0
@@ -162,22 +173,35 @@ class TRPOAgent:
         history = []
         while max_iterations is None or i < max_iterations:
             say("Rollout")
+            inj = {}
+            if draws is not None:
+                ru, au, me = draws(i)
+                inj = {"reset_uniforms": ru, "action_uniforms": au, "max_episodes_per_env": me}
             n, n_paths = eng.rollout_cartpole(n_envs=n_envs, n_timesteps=cfg["episodes_per_roll"],
                                               max_pathlength=cfg["max_steps"], seed=seed * 1000003 + i,
-                                              train=self.train)                          # :96-100
+                                              train=self.train, **inj)                   # :96-100
             eng.rollout_to_batch()                                                       # :108-122
-            self.vf.predict_engine(eng)                                                  # :103
-            eng.compute_advantages_device(cfg["gamma"])                                  # :104-117
+            have_base = self.vf.predict_engine(eng)                                      # :103
+            if record:
+                rb = self.vf.net.predict(np.empty(n, np.float64)) if have_base else np.zeros(n)
+                r_ret, r_adv = np.empty(n), np.empty(n)
+                eng.compute_advantages_device(cfg["gamma"], returns_out=r_ret, advant_out=r_adv)
+            else:
+                eng.compute_advantages_device(cfg["gamma"])                              # :104-117
             ep = eng.rollout_fetch_stats()
             episoderewards = np.add.reduceat(ep["rewards"], np.flatnonzero(ep["starts"]))   # :131
             say("\n********** Iteration %i ************" % i)
             rec = {"iteration": i, "steps": n, "paths": n_paths, "train": self.train,
-                   "reward_mean": float(episoderewards.mean())}
+                   "reward_mean": float(episoderewards.mean()), "end_count": self.end_count}
+            if record:
+                rec.update({"rollout": eng.rollout_fetch(), "baseline": rb, "returns": r_ret, "advantages": r_adv})
             if episoderewards.mean() > 1.1 * 500:                                        # :135-136
                 self.train = False
+            rec["train"] = self.train                    # whether this iteration updates the policy
             if not self.train:                                                           # :137-141
                 say("Episode mean: %f" % episoderewards.mean())
                 self.end_count += 1
+                rec["end_count"] = self.end_count
                 if self.end_count > 100:
                     history.append(rec)
                     break
@@ -200,7 +224,8 @@ class TRPOAgent:
                     say(k + ": " + " " * (40 - len(k)) + str(v))
                 rec.update({"entropy": float(st["ent_after"]), "kl": float(st["kl_after"]),
                             "surr": float(st["surr_after"]), "explained_variance": float(exp),
-                            "reverted": bool(st["reverted"]), "k": int(st["k"]), "episodes": numeptotal})
+                            "reverted": bool(st["reverted"]), "k": int(st["k"]), "episodes": numeptotal,
+                            "cg_iters": int(st["cg_iters"]), "shs": float(st["shs"])})
                 history.append(rec)
                 if st["ent_after"] != st["ent_after"]:                                    # :172-173
                     rec["nan_exit"] = True

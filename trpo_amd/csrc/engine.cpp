@@ -161,7 +161,10 @@ struct trpo_engine {
     return static_cast<T*>(ptr);
   }
 
-  void use() { HIPCHECK(hipSetDevice(device)); }
+  void use() {
+    HIPCHECK(hipSetDevice(device));
+    if (!har_slots.empty()) rewind_har();
+  }
 
   const float* act_in(int l) const { return l == 0 ? X : H[l]; }
 
@@ -487,6 +490,7 @@ struct trpo_engine {
     for (void* ptr : roll.mem) (void)hipFree(ptr);
     roll.mem.clear();
     drop_graph();
+    free_har_slots();
     if (hsc) (void)hipHostFree(hsc);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
@@ -515,25 +519,89 @@ struct trpo_engine {
                                                                      : hipMemcpyDeviceToHost,
                             stream));
     HIPCHECK(hipStreamSynchronize(stream));
+    har_pending = false;
+    check_har();
   }
 
-  void host_allreduce(void* buf, size_t bytes, size_t count, int dtype) {
-    host_ar_buf.resize(bytes);
-    HIPCHECK(hipMemcpyAsync(host_ar_buf.data(), buf, bytes, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
-    REQUIRE(host_ar(host_ar_buf.data(), (int64_t)count, dtype, host_ar_ctx) == 0, "host all-reduce callback failed");
-    HIPCHECK(hipMemcpyAsync(buf, host_ar_buf.data(), bytes, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+  // Host test transport, stream-ordered: D2H into a pinned slot, a host node that calls the
+  // caller's all-reduce (e.g. gloo) on it, H2D back.  No host synchronisation, so it is captured
+  // into the update hipGraph like an RCCL call.  Each call site owns its own slot (a replayed graph
+  // keeps the pointers it captured); a callback failure is latched and raised at the next sync.
+  struct HostArSlot {
+    trpo_engine* e;
+    void* host;
+    size_t bytes;
+    int64_t count;
+    int dtype;
+  };
+  std::vector<HostArSlot*> har_slots;
+  size_t har_next = 0;          // slot cursor, rewound by every update / standalone call
+  int har_failed = 0;           // written by the host node, read after a stream sync
+  static void host_ar_node(void* arg) {
+    HostArSlot* s = static_cast<HostArSlot*>(arg);
+    if (s->e->host_ar(s->host, s->count, s->dtype, s->e->host_ar_ctx) != 0) s->e->har_failed = 1;
   }
+  HostArSlot* har_slot(size_t bytes, int64_t count, int dtype) {
+    if (har_next == har_slots.size()) {
+      auto* s = new HostArSlot{this, nullptr, 0, 0, 0};
+      har_slots.push_back(s);
+    }
+    HostArSlot* s = har_slots[har_next++];
+    if (s->bytes < bytes) {
+      if (s->host) HIPCHECK(hipHostFree(s->host));
+      s->host = nullptr;
+      HIPCHECK(hipHostMalloc(&s->host, bytes, hipHostMallocDefault));
+      s->bytes = bytes;
+    }
+    s->count = count;
+    s->dtype = dtype;
+    return s;
+  }
+  void free_har_slots() {
+    for (HostArSlot* s : har_slots) {
+      if (s->host) (void)hipHostFree(s->host);
+      delete s;
+    }
+    har_slots.clear();
+    har_next = 0;
+  }
+  void check_har() {
+    if (har_failed) {
+      har_failed = 0;
+      throw std::runtime_error("host all-reduce callback failed");
+    }
+  }
+  void host_allreduce(void* buf, size_t bytes, size_t count, int dtype) {
+    HostArSlot* s = har_slot(bytes, (int64_t)count, dtype);
+    HIPCHECK(hipMemcpyAsync(s->host, buf, bytes, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipLaunchHostFunc(stream, host_ar_node, s));
+    HIPCHECK(hipMemcpyAsync(buf, s->host, bytes, hipMemcpyHostToDevice, stream));
+    har_pending = true;
+  }
+  bool har_pending = false;     // a host node may still read its slot
+  size_t har_graph_end = 0;     // slots [0, har_graph_end) belong to the captured update graph
+  // every C-ABI entry: slots are reused from the first one the update graph does not own, once no
+  // enqueued host node can still read them
+  void rewind_har() {
+    if (har_pending) {
+      HIPCHECK(hipStreamSynchronize(stream));
+      har_pending = false;
+    }
+    check_har();
+    har_next = har_graph_end;
+  }
+  bool multi_rank() const { return comm != nullptr || (host_ar && world > 1); }
+  // RCCL when a communicator exists (any world size, world = 1 included: trpo_comm_init always
+  // creates one), else the host transport for world > 1, else nothing to reduce
   void allreduce_f32(float* buf, size_t count) {
-    if (world <= 1) return;
+    if (!multi_rank()) return;
     Scope sp(this, "allreduce");
-    if (host_ar) return host_allreduce(buf, count * sizeof(float), count, TRPO_F32);
+    if (!comm) return host_allreduce(buf, count * sizeof(float), count, TRPO_F32);
     NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, stream));
   }
   void allreduce_f64(double* buf, size_t count) {
-    if (world <= 1) return;
-    if (host_ar) return host_allreduce(buf, count * sizeof(double), count, TRPO_F64);
+    if (!multi_rank()) return;
+    if (!comm) return host_allreduce(buf, count * sizeof(double), count, TRPO_F64);
     NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream));
   }
 
@@ -1016,6 +1084,8 @@ struct trpo_engine {
   void fetch_scalars() {
     HIPCHECK(hipMemcpyAsync(hsc, sc, sizeof(UpdScalars), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
+    har_pending = false;
+    check_har();
   }
 
   // loss(th) at a device parameter vector, without touching the prepared cache
@@ -1042,6 +1112,20 @@ struct trpo_engine {
     check_launch();
     prepared = false;
     have_returns = true;
+  }
+
+  // adv = (adv - mean)/(std + 1e-8) over all ranks (trpo_inksci.py:115-117), device arrays on this
+  // engine's stream; the same kernels and sums as compute_advantages
+  void standardize(double* adv, float* adv32, int64_t cnt, int64_t cnt_global) {
+    const double inv_n = 1.0 / (double)cnt_global;
+    launch_adv_center_partials(adv, nullptr, adv, cnt, partA, stream);
+    launch_sum_finish(partA, dscal + 6, stream);
+    allreduce_f64(dscal + 6, 1);
+    launch_adv_sq_partials(adv, cnt, dscal + 6, inv_n, partA, stream);
+    launch_sum_finish(partA, dscal + 7, stream);
+    allreduce_f64(dscal + 7, 1);
+    launch_adv_normalize(adv, adv32, cnt, dscal + 6, dscal + 7, inv_n, stream);
+    check_launch();
   }
 
   // 1 - var(y - ypred)/var(y) with y = returns, ypred = baseline (utils.py:208-211), f64 over all ranks
@@ -1104,6 +1188,9 @@ struct trpo_engine {
   // and replays, later ones replay.  Host flags the prefix leaves behind are restored after a replay.
   struct GraphKey {
     int64_t n, n_global;
+    const void* comm;   // the communicator / host transport the all-reduces were captured with
+    const void* host_ar;
+    int rank, world;
     int cg_iters, adv, baseline;
     float tol, damping;
     double gamma;
@@ -1114,6 +1201,10 @@ struct trpo_engine {
     std::memset(&k, 0, sizeof k);
     k.n = n;
     k.n_global = n_global;
+    k.comm = comm;
+    k.host_ar = (const void*)host_ar;
+    k.rank = rank;
+    k.world = world;
     k.cg_iters = prm.cg_iters;
     k.adv = prm.compute_advantages != 0;
     k.baseline = have_baseline;
@@ -1130,12 +1221,17 @@ struct trpo_engine {
     bool prepared, w3_valid, chain_w_valid, have_returns;
   } upd_flags{};
   void drop_graph() {
-    if (upd_exec) (void)hipGraphExecDestroy(upd_exec);
+    if (upd_exec) {
+      if (har_graph_end) (void)hipStreamSynchronize(stream);   // its host nodes may still be pending
+      (void)hipGraphExecDestroy(upd_exec);
+    }
     upd_exec = nullptr;
     upd_key_seen = false;
+    har_graph_end = 0;
   }
   void run_prefix(const trpo_update_params& prm) {
-    const bool graphable = g_options.graphs != 0 && !prof && world <= 1 && !graphs_broken;
+    // multi-rank engines capture their all-reduces too (RCCL calls or the host transport's nodes)
+    const bool graphable = g_options.graphs != 0 && !prof && !graphs_broken;
     if (!graphable) {
       update_prefix(prm);
       return;
@@ -1144,6 +1240,7 @@ struct trpo_engine {
     const bool same = upd_key_seen && std::memcmp(&key, &upd_key, sizeof key) == 0;
     if (same && upd_exec) {
       HIPCHECK(hipGraphLaunch(upd_exec, stream));
+      if (har_graph_end) har_pending = true;
       prepared = upd_flags.prepared;
       w3_valid = upd_flags.w3_valid;
       chain_w_valid = upd_flags.chain_w_valid;
@@ -1152,6 +1249,7 @@ struct trpo_engine {
     }
     if (!same) {
       drop_graph();
+      har_next = 0;
       update_prefix(prm);
       upd_key = key;
       upd_key_seen = true;
@@ -1160,6 +1258,7 @@ struct trpo_engine {
     // capture (the cache is rebuilt inside the graph, so the prefix must not skip prepare())
     prepared = false;
     hipGraph_t graph = nullptr;
+    har_next = 0;
     HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
       update_prefix(prm);
@@ -1181,7 +1280,9 @@ struct trpo_engine {
       return;
     }
     upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns};
+    har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
+    if (har_graph_end) har_pending = true;
   }
 
   void update(const trpo_update_params& prm, trpo_update_stats* st) {
@@ -1259,6 +1360,8 @@ int trpo_synchronize(trpo_engine* e) {
     REQUIRE(e, "engine is NULL");
     e->use();
     HIPCHECK(hipStreamSynchronize(e->stream));
+    e->har_pending = false;
+    e->check_har();
   });
 }
 
@@ -1283,13 +1386,15 @@ int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world) {
       NCCLCHECK(ncclCommDestroy(e->comm));
       e->comm = nullptr;
     }
+    e->drop_graph();
     e->rank = rank;
     e->world = world;
-    if (world > 1) {
-      ncclUniqueId uid;
-      std::memcpy(&uid, id, sizeof uid);
-      NCCLCHECK(ncclCommInitRank(&e->comm, world, uid, rank));
-    }
+    e->host_ar = nullptr;
+    // world = 1 creates a one-rank communicator as well: every all-reduce then runs through RCCL
+    // (an identity), which exercises that path on a single GPU
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    NCCLCHECK(ncclCommInitRank(&e->comm, world, uid, rank));
   });
 }
 
@@ -1297,6 +1402,12 @@ int trpo_comm_set_host_allreduce(trpo_engine* e, trpo_allreduce_cb cb, void* ctx
   return guarded([&] {
     REQUIRE(e && cb, "NULL argument");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    e->use();
+    e->drop_graph();
+    if (e->comm) {
+      NCCLCHECK(ncclCommDestroy(e->comm));
+      e->comm = nullptr;
+    }
     e->host_ar = cb;
     e->host_ar_ctx = ctx;
     e->rank = rank;
@@ -1411,6 +1522,57 @@ int trpo_compute_advantages(trpo_engine* e, double gamma, double* returns_out, d
     e->compute_advantages(gamma);
     if (returns_out) e->copy_out(returns_out, e->returns, (size_t)e->n * sizeof(double), mem);
     if (advant_out) e->copy_out(advant_out, e->adv64, (size_t)e->n * sizeof(double), mem);
+  });
+}
+
+int trpo_standardize(trpo_engine* e, double* adv, int64_t n, int64_t n_global, float* adv32_out, int mem) {
+  return guarded([&] {
+    REQUIRE(adv, "adv is NULL");
+    REQUIRE(n >= 0 && n_global >= n, "need 0 <= n <= n_global");
+    REQUIRE(e || n_global == n, "n_global != n needs an engine (its communicator sums the ranks)");
+    if (e) e->use();
+    if (n_global == 0) return;
+    hipStream_t s = e ? e->stream : nullptr;
+    std::vector<void*> tmps;
+    auto dev = [&](size_t bytes) {
+      void* ptr = nullptr;
+      HIPCHECK(hipMalloc(&ptr, std::max<size_t>(bytes, 16)));
+      tmps.push_back(ptr);
+      return ptr;
+    };
+    try {
+      const bool host = mem != TRPO_MEM_DEVICE;
+      double* da = adv;
+      float* d32 = adv32_out;
+      if (host) {
+        da = static_cast<double*>(dev((size_t)n * sizeof(double)));
+        copy_in(da, adv, (size_t)n * sizeof(double), TRPO_MEM_HOST, s);
+        d32 = adv32_out ? static_cast<float*>(dev((size_t)n * sizeof(float))) : nullptr;
+      }
+      if (e) {
+        e->standardize(da, d32, n, n_global);
+      } else {
+        double* part = static_cast<double*>(dev(kRedBlocks * sizeof(double)));
+        double* sums = static_cast<double*>(dev(2 * sizeof(double)));
+        const double inv_n = 1.0 / (double)n;
+        launch_adv_center_partials(da, nullptr, da, n, part, s);
+        launch_sum_finish(part, sums, s);
+        launch_adv_sq_partials(da, n, sums, inv_n, part, s);
+        launch_sum_finish(part, sums + 1, s);
+        launch_adv_normalize(da, d32, n, sums, sums + 1, inv_n, s);
+        check_launch();
+      }
+      if (host) {
+        copy_out(adv, da, (size_t)n * sizeof(double), TRPO_MEM_HOST, s);
+        if (adv32_out) copy_out(adv32_out, d32, (size_t)n * sizeof(float), TRPO_MEM_HOST, s);
+      }
+      HIPCHECK(hipStreamSynchronize(s));
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      for (void* t : tmps) (void)hipFree(t);
+      throw;
+    }
+    for (void* t : tmps) HIPCHECK(hipFree(t));
   });
 }
 
@@ -1740,7 +1902,7 @@ int trpo_get_feed_view(trpo_engine* e, trpo_feed_view* v) {
     v->old_dist = e->old;
     v->ld_old = e->wp[e->L];
     v->episode_starts = e->have_rewards ? e->starts : nullptr;
-    v->returns = e->returns;
+    v->returns = e->have_returns ? e->returns : nullptr;   // stale until the advantages are computed
     v->baseline = e->baseline;
   });
 }

@@ -165,7 +165,7 @@ __global__ void adv_normalize_kernel(double* adv, float* adv32, int64_t n, const
        i += (int64_t)gridDim.x * blockDim.x) {
     const double a = (adv[i] - mean) / denom;
     adv[i] = a;
-    adv32[i] = (float)a;
+    if (adv32) adv32[i] = (float)a;
   }
 }
 

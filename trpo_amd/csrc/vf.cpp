@@ -210,8 +210,8 @@ struct trpo_vf {
   }
 
   void allreduce_grad() {
-    if (world <= 1) return;
-    if (host_ar) {
+    if (!comm && !(host_ar && world > 1)) return;
+    if (!comm) {
       std::vector<float> h((size_t)P);
       HIPCHECK(hipMemcpyAsync(h.data(), grad, P * sizeof(float), hipMemcpyDeviceToHost, stream));
       HIPCHECK(hipStreamSynchronize(stream));
@@ -529,11 +529,10 @@ int trpo_vf_comm_init(trpo_vf* e, const uint8_t id[128], int rank, int world) {
     e->rank = rank;
     e->world = world;
     e->host_ar = nullptr;
-    if (world > 1) {
-      ncclUniqueId uid;
-      std::memcpy(&uid, id, sizeof uid);
-      NCCLCHECK(ncclCommInitRank(&e->comm, world, uid, rank));
-    }
+    // world = 1 creates a one-rank communicator too (the RCCL path on a single GPU)
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    NCCLCHECK(ncclCommInitRank(&e->comm, world, uid, rank));
   });
 }
 
@@ -541,6 +540,11 @@ int trpo_vf_comm_set_host_allreduce(trpo_vf* e, trpo_allreduce_cb cb, void* ctx,
   return guarded([&] {
     REQUIRE(e && cb, "NULL argument");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    e->use();
+    if (e->comm) {
+      NCCLCHECK(ncclCommDestroy(e->comm));
+      e->comm = nullptr;
+    }
     e->host_ar = cb;
     e->host_ar_ctx = ctx;
     e->rank = rank;

@@ -224,6 +224,11 @@ class Engine:
               "trpo_compute_advantages")
         return ret, adv
 
+    def standardize(self, adv, n_global: Optional[int] = None, adv32_out=None):
+        """trpo_inksci.py:115-117 on the device, summed over the engine's ranks: adv (f64 [n]) is
+        standardised in place (a numpy array is updated too); returns adv."""
+        return _standardize(self._h, adv, n_global, adv32_out)
+
     # ------------------------------------------------------------------ graph outputs
     def losses(self):
         out = (ctypes.c_float * 3)()
@@ -431,6 +436,26 @@ def discount_device(x, gamma: float, episode_starts=None) -> np.ndarray:
         oa = _Arg(out, np.float64, writable=True)
     check(lib.trpo_discount(xa.ptr, st.ptr, n, float(gamma), oa.ptr, xa.mem), "trpo_discount")
     return out
+
+
+def _standardize(handle, adv, n_global, adv32_out):
+    if not _is_torch(adv):
+        if not (isinstance(adv, np.ndarray) and adv.dtype == np.float64 and adv.flags.c_contiguous):
+            raise TypeError("standardize: adv must be a C-contiguous float64 array (updated in place)")
+    a = _Arg(adv, np.float64, writable=True)
+    n = int(adv.numel()) if _is_torch(adv) else int(adv.size)
+    o = _Arg(adv32_out, np.float32, (n,), writable=True) if adv32_out is not None else _Arg(None, np.float32)
+    if o.ptr is not None and o.mem != a.mem:
+        raise ValueError("standardize: adv and adv32_out must live in the same memory")
+    check(lib.trpo_standardize(handle, a.ptr, n, n if n_global is None else int(n_global), o.ptr, a.mem),
+          "trpo_standardize")
+    return adv
+
+
+def standardize_device(adv, adv32_out=None):
+    """adv = (adv - mean)/(std + 1e-8) (trpo_inksci.py:115-117) in place on the current GPU, one
+    process (engine-free)."""
+    return _standardize(None, adv, None, adv32_out)
 
 
 def cg_callback(f_Ax, b, cg_iters=10, residual_tol=1e-10):
