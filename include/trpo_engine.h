@@ -180,8 +180,10 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * gradients; 1..3 = split-bf16 tile for fan_out > 128), "fused_head" and "head_bwd"
  * (last-layer fusions; read when an engine is created), "chain" (fused FVP chain: 0 off, 1 auto),
  * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
- * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph on a
- * single-rank engine; results are bit-identical to eager launches).  Process-wide. */
+ * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph, all-reduces
+ * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
+ * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions).
+ * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);
 

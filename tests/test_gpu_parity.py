@@ -501,3 +501,43 @@ def test_update_bench_dims_vs_oracle(gpu_available, obs, hidden, A, n):
     assert st["shs"] == pytest.approx(r.shs, rel=REL)
     assert_vec_close(eng.get_flat(), r.theta_new, REL, "theta_new")
     eng.close()
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (128, [256, 256], 18, 3001),       # C4 dims (the bench workload's layer shapes), ragged last tile
+    (37, [200, 192], 17, 777),         # hidden 192: three of the four waves' column blocks, 17 actions
+    (9, [64, 160, 256], 32, 1500),     # depth 3, A = 32 (one full action tile)
+    (128, [256], 20, 64),              # the reference's depth (one hidden layer), fewer rows than a split
+])
+def test_fused_tail_vs_oracle_and_per_layer(gpu_available, obs, hidden, A, n):
+    """tail.hip (head R-forward + R-softmax + R-backward + last-layer weight R-gradient in one
+    launch, E recomputed from D_L) against the float64 oracle and against the per-layer kernels it
+    replaces (option tail = 0), for the FVP and a whole update (trpo_inksci.py:56-70,144-158)."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + A)
+    v = np.random.RandomState(n).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
+    r = O.trpo_update(dd["theta"].astype(np.float64), O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]),
+                      spec, np.float64, 10, 0.0)
+    saved = get_option("tail")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("tail", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            hv = e.fvp(v, 0.0)
+            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out[mode] = (hv, st, e.get_flat())
+            e.close()
+    finally:
+        set_option("tail", saved)
+    for mode in (1, 0):
+        hv, st, th = out[mode]
+        assert_vec_close(hv, ref, REL, f"Hv tail={mode} {obs} {hidden} {A}")
+        assert st["k"] == r.k
+        assert_vec_close(th, r.theta_new, REL, f"theta tail={mode} {obs} {hidden} {A}")
+    assert_vec_close(out[1][0], out[0][0], REL, "fused tail vs per-layer Hv")

@@ -104,6 +104,12 @@ struct trpo_engine {
     if (first && count > 0)
       HIPCHECK(hipMemsetAsync(first, 0, (size_t)count * kAmaxSlot * sizeof(unsigned), stream));
   }
+  uint16_t* tail_planes = nullptr;   // head planes of the fused FVP tail (tail.hip), [2][2][32][kTailK]
+  // the fused last-layer tail: f16 split, last hidden width in (128, 256], 17..32 actions
+  bool use_tail() const {
+    return g_options.tail != 0 && f16 && split_on() && L >= 2 && !fused_head && !head_bwd &&
+           tail_eligible(wp[L - 1], wp[L]) && w[L] <= 32;
+  }
   bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
   bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
@@ -301,6 +307,7 @@ struct trpo_engine {
     head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
     f16 = g_options.split_f16 != 0;
     amax = dalloc<unsigned>((size_t)(1 + 7 * kMaxLayers) * kAmaxSlot);
+    if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
     // allocated last: the big activation buffers keep the placement the kernels were tuned on
     stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
@@ -858,8 +865,9 @@ struct trpo_engine {
     split_parts(false, true, false, true, WF, WF3, skip, "split_v");
     am_reset(am_rh(0), L);
     am_reset(am_rd(0), L);
-    // R-forward
-    const int Lf = fused_head ? L - 1 : L;
+    // R-forward (the fused tail takes the last layer's)
+    const bool tail = use_tail();
+    const int Lf = (fused_head || tail) ? L - 1 : L;
     for (int l = 0; l < Lf; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       float* Vpart = WF[l] + (size_t)wp[l] * wp[l + 1];
@@ -961,7 +969,54 @@ struct trpo_engine {
       check_launch();
       if (f16) launch_amax(RD[l - 1], n, w[l], wp[l], am_rd(l - 1), stream);
     }
-    const bool tail_fused = fused_head || head_bwd;
+    if (tail) {
+      const int l = L - 1;
+      TailPackArgs tp{};
+      tp.theta = theta;
+      tp.v = v;
+      tp.off_w = offW[l];
+      tp.a = w[l];
+      tp.b = w[l + 1];
+      tp.am_w = am_w(l);
+      tp.am_v = am_v(l);
+      tp.out = tail_planes;
+      TailArgs ta{};
+      ta.rows = (int)n;
+      ta.a = w[l];
+      ta.b = w[l + 1];
+      ta.apad = wp[l];
+      ta.bpad = wp[l + 1];
+      ta.RH = RH[l];
+      ta.H = H[l];
+      ta.P = Pm;
+      ta.DL = D[l];
+      ta.c = v + offb[l];
+      ta.WV16 = tail_planes;
+      ta.WT16 = WB3[l];
+      ta.VT16 = WB3[l] + 3 * plane3_b(l);
+      ta.bplane = (int64_t)plane3_b(l);
+      ta.am_rh = am_rh(l);
+      ta.am_d = am_d(l);
+      ta.am_w = am_w(l);
+      ta.am_v = am_v(l);
+      ta.am_out = am_rd(l - 1);
+      ta.RDout = RD[l - 1];
+      ta.invN = 1.0 / (double)n_global;
+      ta.splits = active_splits;
+      ta.rows_per_split = rows_per_split;
+      ta.slab = slab;
+      ta.slab_stride = slab_stride;
+      ta.off_w = offW[l];
+      ta.off_b = offb[l];
+      ta.skip = skip;
+      char tag[32];
+      std::snprintf(tag, sizeof tag, "fvp_tail_l%d", l);
+      Scope sp(this, tag);
+      launch_tail_pack(tp, stream);
+      launch_fvp_tail(ta, stream);
+      check_launch();
+    }
+    const bool tail_fused = fused_head || head_bwd || tail;
     // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
     for (int l = tail_fused ? L - 2 : L - 1; l >= 1; --l) {
       RowGemmArgs a = row_args(w[l], wp[l]);
@@ -2088,6 +2143,8 @@ static int* option_slot(const std::string& k) {
   if (k == "split_f16") return &g_options.split_f16;
   if (k == "split_min_k") return &g_options.split_min_k;
   if (k == "graphs") return &g_options.graphs;
+  if (k == "tail") return &g_options.tail;
+  if (k == "stagger") return &g_options.stagger;
   throw ArgError("unknown option " + k);
 }
 

@@ -23,7 +23,9 @@ struct Options {
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
   int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
-  int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph (single rank)
+  int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
+  int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
+  int stagger;     // row GEMM 2-blocks-per-CU configs: start-time stagger of co-resident blocks (experiment)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -105,6 +107,7 @@ struct RowGemmArgs {
   RowEpi epi;
   RowEpiArgs ea;
   int f16 = 0;         // split path: 1 = two scaled f16 planes / 3 products, 0 = three bf16 planes / 6
+  int stagger = 0;     // row_cfg experiments: the first round's second co-resident blocks sleep ~4 us x stagger
 };
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
@@ -376,6 +379,49 @@ int chain_max_tiles(int max_hidden);   // register tiles for a max hidden width 
 void launch_fvp_chain(const ChainArgs& a, int otm, hipStream_t s);
 void launch_chain_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
                       hipStream_t s);
+}  // namespace trpo
+
+namespace trpo {
+// ---------------------------------------------------------------------------
+// Fused last-layer FVP tail (tail.hip), for the f16-split engine when the last hidden width is
+// in (128, 256] (a multiple of 32) and n_actions <= 32.  Per 32-row tile of a split-K slab:
+//   RZ = RH W + H V + c ; RD_L = R-softmax-reverse(RZ)             (head R-forward, kRHead)
+//   RD_out = (RD_L W^T + D_L V^T)(1-H^2) - 2 (D_L W^T) H RH        (R-backward, E recomputed)
+//   slab  += RH^T D_L + H^T RD_L ; bias += colsum RD_L              (weight R-gradient)
+// reading RH and H once.  All products on the scaled f16 hi+lo split.
+// ---------------------------------------------------------------------------
+constexpr int kTailK = 256;   // max hidden width of the tail (head planes are [2][2][32][kTailK])
+struct TailArgs {
+  int rows, a, b, apad, bpad;
+  const float* RH;            // [rows][apad]  R{h} of the last hidden layer
+  const float* H;             // [rows][apad]  its tanh activations
+  const float* P;             // [rows][bpad]  softmax at theta
+  const float* DL;            // [rows][bpad]  KL_ff plain logit delta D_{L-1}
+  const float* c;             // [b]           tangent bias of the last layer
+  const uint16_t* WV16;       // head planes [mat W,V][plane hi,lo][32 j][kTailK k] (launch_tail_pack)
+  const uint16_t* WT16;       // R-backward planes of W^T: [plane][apad n][32 k], plane stride bplane
+  const uint16_t* VT16;       // ... of V^T
+  int64_t bplane;
+  const unsigned *am_rh, *am_d, *am_w, *am_v;   // running-max slots of RH, D_L, W, V
+  unsigned* am_out;           // running max |RD_out|
+  float* RDout;               // [rows][apad]  R-delta into the last hidden layer (RD_{L-2})
+  double invN;
+  int splits, rows_per_split; // rows_per_split % 32 == 0
+  float* slab;
+  int64_t slab_stride, off_w, off_b;
+  const int* skip;
+};
+struct TailPackArgs {
+  const float* theta;
+  const float* v;
+  int64_t off_w;              // flat offset of W_{L-1} [a][b]
+  int a, b;
+  const unsigned *am_w, *am_v;
+  uint16_t* out;              // [2][2][32][kTailK]
+};
+bool tail_eligible(int apad, int bpad);   // (128, kTailK] multiple of 32; bpad in (16, 32]
+void launch_tail_pack(const TailPackArgs& p, hipStream_t s);
+void launch_fvp_tail(const TailArgs& a, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
