@@ -77,7 +77,8 @@ typedef struct trpo_update_stats {
 
 /* Build an engine for the categorical tanh-MLP policy of trpo_inksci.py:38-40
  * (hidden widths as a list; the reference is the depth-1 case {64}) with room
- * for `max_rows` states on GPU `device`.  n_actions <= 32. */
+ * for `max_rows` states on GPU `device`.  n_actions <= 128 (the reference's softmax_classifier has
+ * no bound; a softmax row spans up to 4 x 32 lanes here). */
 int trpo_create(trpo_engine** out, int obs_dim, const int* hidden, int n_hidden, int n_actions,
                 int64_t max_rows, int device);
 void trpo_destroy(trpo_engine* e);

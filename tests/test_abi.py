@@ -59,7 +59,7 @@ def test_errors_are_reported_not_crashes():
     import ctypes
     from trpo_amd import _lib
     h = ctypes.c_void_p()
-    rc = _lib.lib.trpo_create(ctypes.byref(h), 4, (ctypes.c_int * 1)(64), 1, 40, 100, 0)   # A > 32
+    rc = _lib.lib.trpo_create(ctypes.byref(h), 4, (ctypes.c_int * 1)(64), 1, 200, 100, 0)   # A > 128
     assert rc != 0
     assert b"n_actions" in _lib.lib.trpo_last_error()
 

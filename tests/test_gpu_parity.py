@@ -541,3 +541,32 @@ def test_fused_tail_vs_oracle_and_per_layer(gpu_available, obs, hidden, A, n):
         assert st["k"] == r.k
         assert_vec_close(th, r.theta_new, REL, f"theta tail={mode} {obs} {hidden} {A}")
     assert_vec_close(out[1][0], out[0][0], REL, "fused tail vs per-layer Hv")
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (16, [64, 64], 64, 2000),          # f32 MFMA path, two 32-column softmax tiles per row
+    (32, [256, 256], 100, 1500),       # f16-split path (the fused tail takes <= 32 actions: per-layer)
+    (11, [64], 33, 777),               # one action past a single tile
+])
+def test_many_actions_vs_oracle(gpu_available, obs, hidden, A, n):
+    """More than 32 actions (trpo_inksci.py:40's softmax_classifier(action_dim) has no bound):
+    losses, policy gradient, Hv and a whole update against the float64 oracle."""
+    from trpo_amd import Engine, UpdateParams
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=A)
+    th = dd["theta"].astype(np.float64)
+    e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+    e.set_flat(dd["theta"])
+    e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+    ref_l = O.losses(th, dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    assert np.allclose(e.losses(), ref_l, rtol=1e-5, atol=1e-7)
+    assert_vec_close(e.action_dist(), O.action_dist(th, dd["X"], spec), REL, "action_dist")
+    assert_vec_close(e.policy_grad(), O.policy_grad(th, dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec),
+                     REL, f"g A={A}")
+    v = np.random.RandomState(A).standard_normal(spec.n_params).astype(np.float32)
+    assert_vec_close(e.fvp(v, 0.0), O.fvp_undamped(th, dd["X"], v.astype(np.float64), spec), REL, f"Hv A={A}")
+    st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+    r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
+    assert st["k"] == r.k
+    assert_vec_close(e.get_flat(), r.theta_new, REL, f"theta A={A}")
+    e.close()

@@ -217,16 +217,14 @@ struct trpo_engine {
   void init(int obs, const int* hidden, int nh, int A, int64_t max_rows, int dev) {
     REQUIRE(obs > 0 && A > 0 && nh >= 0 && max_rows > 0, "invalid policy dimensions");
     REQUIRE(nh + 1 <= kMaxLayers, "too many layers");
-    REQUIRE(A <= 32, "n_actions must be <= 32 (one wave-half softmax row)");
+    REQUIRE(A <= 32 * kMaxHeadTiles, "n_actions must be <= 128 (softmax rows of up to 4 x 32 lanes)");
     REQUIRE(max_rows < (int64_t(1) << 31), "max_rows must fit in int32 row indices");
+    for (int i = 0; i < nh; ++i) REQUIRE(hidden[i] > 0, "hidden widths must be positive");
     device = dev;
     use();
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     w.push_back(obs);
-    for (int i = 0; i < nh; ++i) {
-      REQUIRE(hidden[i] > 0, "hidden widths must be positive");
-      w.push_back(hidden[i]);
-    }
+    for (int i = 0; i < nh; ++i) w.push_back(hidden[i]);
     w.push_back(A);
     L = (int)w.size() - 1;
     for (int v : w) wp.push_back(pad4(v));
@@ -1985,6 +1983,7 @@ int trpo_act(trpo_engine* e, const float* states, int64_t n, const double* unifo
   return guarded([&] {
     REQUIRE(e && states && n >= 0, "bad argument");
     REQUIRE(!train || uniforms, "train = 1 needs uniforms (cat_sample's np.random.rand)");
+    REQUIRE(e->w[e->L] <= 64, "act: n_actions must be <= 64 (one wave per state)");
     e->use();
     if (n == 0) return;
     const int obs = e->w[0], A = e->w[e->L];

@@ -156,63 +156,108 @@ __device__ __forceinline__ void epi_store(const RowEpiArgs& e, size_t idx, float
 }
 
 // ---------------------------------------------------------------------------
-// row-wise softmax-head epilogues.  The 32 columns of one row live on the 32
-// lanes of one wave half (col = lane & 31); reductions are xor-shuffles of
-// width 32.  Requires n_actions <= 32.
+// row-wise softmax-head epilogues.  The row's columns live on the 32 lanes of one wave half, TN
+// per lane (col = 32 t + (lane & 31), t < TN): n_actions <= 32 TN.  Row reductions sum the TN
+// values of a lane first, then xor-shuffle over the 32 lanes.
 // ---------------------------------------------------------------------------
-template <int EPI>
-__device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowvalid, int col, int A,
-                                        float v, float& m0, float& m1, float& m2) {
+template <int EPI, int TN>
+__device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowvalid, int lr, int A,
+                                        const float (&v)[TN], float& m0, float& m1, float& m2) {
   // `row` is already clamped into [0, M); loads go to clamped (valid) addresses
   // unconditionally and are masked by selects, so hipcc keeps them in flight.
-  const bool real = col < A;
-  const int colc = col < e.ldo ? col : e.ldo - 1;
-  const size_t idx = (size_t)row * e.ldo + colc;
-  const bool st = rowvalid && col < e.ldo;
+  bool real[TN];
+  size_t idx[TN];
+  bool st[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int col = 32 * t + lr;
+    real[t] = col < A;
+    const int colc = col < e.ldo ? col : e.ldo - 1;
+    idx[t] = (size_t)row * e.ldo + colc;
+    st[t] = rowvalid && col < e.ldo;
+  }
   if constexpr (EPI == (int)RowEpi::kPrepHead || EPI == (int)RowEpi::kLossHead) {
-    const float bias = e.bias[real ? col : 0];
-    const float oldv = e.old[idx];
     const int av = e.act[row];
     const float advv = e.adv[row];
-    // p = softmax(z)   (trpo_inksci.py:40)
-    const float z = real ? v + bias : -INFINITY;
-    const float m = hmax32(z);
-    const float ex = real ? expf(z - m) : 0.0f;
-    const float ssum = hsum32(ex);
-    const float p = ex / ssum;
+    float z[TN], oldv[TN];
+    float zm = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const float bias = e.bias[real[t] ? 32 * t + lr : 0];
+      oldv[t] = e.old[idx[t]];
+      // p = softmax(z)   (trpo_inksci.py:40)
+      z[t] = real[t] ? v[t] + bias : -INFINITY;
+      zm = fmaxf(zm, z[t]);
+    }
+    const float m = hmax32(zm);
+    float ex[TN], es = 0.0f;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      ex[t] = real[t] ? expf(z[t] - m) : 0.0f;
+      es += ex[t];
+    }
+    const float ssum = hsum32(es);
     const int a = rowvalid ? av : 0;
-    const float old = (rowvalid && real) ? oldv : 0.0f;
-    const float pa = __shfl(p, a, 32);
-    const float olda = __shfl(old, a, 32);
+    float p[TN], old[TN];
+    float pa_l = 0.0f, olda_l = 0.0f;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      p[t] = ex[t] / ssum;
+      old[t] = (rowvalid && real[t]) ? oldv[t] : 0.0f;
+      if (t == (a >> 5)) {
+        pa_l = p[t];
+        olda_l = old[t];
+      }
+    }
+    const float pa = __shfl(pa_l, a & 31, 32);
+    const float olda = __shfl(olda_l, a & 31, 32);
     const float adv = rowvalid ? advv : 0.0f;
-    const double pd = p, od = old;
     // row loss terms (:46-51), accumulated in f64
-    const double klt = hsum32d(real ? od * log((od + (double)kEps) / (pd + (double)kEps)) : 0.0);
-    const double ent = hsum32d(real ? -pd * log(pd + (double)kEps) : 0.0);
+    double klp = 0.0, enp = 0.0;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const double pd = p[t], od = old[t];
+      klp += real[t] ? od * log((od + (double)kEps) / (pd + (double)kEps)) : 0.0;
+      enp += real[t] ? -pd * log(pd + (double)kEps) : 0.0;
+    }
+    const double klt = hsum32d(klp);
+    const double ent = hsum32d(enp);
     const double sur = rowvalid ? (double)pa / (double)olda * (double)adv : 0.0;
-    if (rowvalid && col == 0) {
+    if (rowvalid && lr == 0) {
       e.rowterms[4 * (size_t)row + 0] = sur;
       e.rowterms[4 * (size_t)row + 1] = klt;
       e.rowterms[4 * (size_t)row + 2] = ent;
       e.rowterms[4 * (size_t)row + 3] = 0.0;
     }
     if constexpr (EPI == (int)RowEpi::kPrepHead) {
-      const size_t sidx = (size_t)row * e.ldo + col;
-      if (st) e.out0[sidx] = real ? p : 0.0f;
       // KL_ff plain logit delta (:56-57), cancellation-free:
       //   d_j = (p_j/N) (B_j - sum_k p_k B_k),  B = eps/(p+eps)
-      const double B = real ? (double)kEps / (pd + (double)kEps) : 0.0;
-      const double spB = hsum32d(pd * B);
-      const double dl = real ? pd * e.invN * (B - spB) : 0.0;
+      double B[TN], spBp = 0.0, restp = 0.0;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const double pd = p[t];
+        B[t] = real[t] ? (double)kEps / (pd + (double)kEps) : 0.0;
+        spBp += pd * B[t];
+        restp += (real[t] && 32 * t + lr != a) ? pd : 0.0;
+      }
+      const double spB = hsum32d(spBp);
+      const double rest = hsum32d(restp);   // 1 - p_a
       // surr logit delta (:54): -(adv/(N old_a)) p_a (1[j=a] - p_j)
-      const double rest = hsum32d((real && col != a) ? pd : 0.0);  // 1 - p_a
       const double coef = -(double)adv * e.invN / (double)olda * (double)pa;
-      const double ds = real ? coef * (col == a ? rest : -pd) : 0.0;
-      if (st) {
-        e.out1[sidx] = (float)dl;
-        e.out2[sidx] = (float)ds;
-        m1 = fmaxf(m1, fabsf((float)dl));
-        m2 = fmaxf(m2, fabsf((float)ds));
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int col = 32 * t + lr;
+        const double pd = p[t];
+        const double dl = real[t] ? pd * e.invN * (B[t] - spB) : 0.0;
+        const double ds = real[t] ? coef * (col == a ? rest : -pd) : 0.0;
+        if (st[t]) {
+          const size_t sidx = (size_t)row * e.ldo + col;
+          e.out0[sidx] = real[t] ? p[t] : 0.0f;
+          e.out1[sidx] = (float)dl;
+          e.out2[sidx] = (float)ds;
+          m1 = fmaxf(m1, fabsf((float)dl));
+          m2 = fmaxf(m2, fabsf((float)ds));
+        }
       }
     }
   } else if constexpr (EPI == (int)RowEpi::kRHead) {
@@ -220,21 +265,35 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     //   Rp   = p (Rz - <p,Rz>)
     //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k]
     //   A = p/(p+eps), B = eps/(p+eps)
-    const float bias = e.bias[real ? col : 0];
-    const float pv = e.P[idx];
-    const double rz = real ? (double)(v + bias) : 0.0;
-    const double pd = (rowvalid && real) ? (double)pv : 0.0;
-    const double prz = hsum32d(pd * rz);
-    const double Rp = pd * (rz - prz);
-    const double den = pd + (double)kEps;
-    const double Aa = real ? pd / den : 0.0;
-    const double B = real ? (double)kEps / den : 0.0;
-    const double spB = hsum32d(pd * B);
-    const double sRAB = hsum32d(Rp * Aa * B);
-    const double rd = e.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
-    if (st) {
-      e.out0[(size_t)row * e.ldo + col] = real ? (float)rd : 0.0f;
-      if (real) m0 = fmaxf(m0, fabsf((float)rd));
+    double rz[TN], pd[TN], przp = 0.0;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const float bias = e.bias[real[t] ? 32 * t + lr : 0];
+      const float pv = e.P[idx[t]];
+      rz[t] = real[t] ? (double)(v[t] + bias) : 0.0;
+      pd[t] = (rowvalid && real[t]) ? (double)pv : 0.0;
+      przp += pd[t] * rz[t];
+    }
+    const double prz = hsum32d(przp);
+    double Rp[TN], Aa[TN], B[TN], spBp = 0.0, sRABp = 0.0;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      Rp[t] = pd[t] * (rz[t] - prz);
+      const double den = pd[t] + (double)kEps;
+      Aa[t] = real[t] ? pd[t] / den : 0.0;
+      B[t] = real[t] ? (double)kEps / den : 0.0;
+      spBp += pd[t] * B[t];
+      sRABp += Rp[t] * Aa[t] * B[t];
+    }
+    const double spB = hsum32d(spBp);
+    const double sRAB = hsum32d(sRABp);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const double rd = e.invN * (Rp[t] * (B[t] - spB) + Rp[t] * Aa[t] * Aa[t] + pd[t] * sRAB);
+      if (st[t]) {
+        e.out0[(size_t)row * e.ldo + 32 * t + lr] = real[t] ? (float)rd : 0.0f;
+        if (real[t]) m0 = fmaxf(m0, fabsf((float)rd));
+      }
     }
   }
 }
@@ -262,14 +321,16 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
   const RowEpiArgs& e = args.ea;
   float mx0 = 0.0f, mx1 = 0.0f, mx2 = 0.0f;   // max |stored output| for the f16 operand scales
   if constexpr (epi_is_head(EPI)) {
-    static_assert(WN == 1 && TN == 1, "row-wise head epilogue needs the whole row in one wave half");
-    const int col = n0 + lr;
+    static_assert(WN == 1, "row-wise head epilogue needs the whole row in one wave half");
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        epi_row<EPI>(e, row < M ? row : 0, row < M, col, args.N, acc[tm][0][r], mx0, mx1, mx2);
+        float v[TN];
+#pragma unroll
+        for (int t = 0; t < TN; ++t) v[t] = acc[tm][t][r];
+        epi_row<EPI, TN>(e, row < M ? row : 0, row < M, lr, args.N, v, mx0, mx1, mx2);
       }
   } else {
     const bool fulln = (n0 + BN <= args.Npad);
@@ -1706,8 +1767,11 @@ bool small_k_row(const RowGemmArgs& a) {
 template <int EPI>
 void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
   if constexpr (epi_is_head(EPI)) {
-    if (a.N > 32) throw std::runtime_error("softmax head supports at most 32 actions");
-    if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
+    // one 32-column tile per 32 actions in every lane half (epi_row)
+    if (a.N > 32 * kMaxHeadTiles) throw std::runtime_error("softmax head supports at most 128 actions");
+    if (a.N > 64) launch_row_cfg<4, 1, 2, 4, 16, EPI>(a, s);
+    else if (a.N > 32) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
+    else if (g_options.narrow_pf == 2) launch_row_cfg<4, 1, 2, 1, 16, EPI, 2>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
   } else if (rowgemm_uses_split(a.Npad, a.epi) && !small_k_row(a)) {
     switch (g_options.split_mfma) {

@@ -73,7 +73,8 @@ enum class RowEpi : int {
   kRelu = 8,      // out = max(acc + bias, 0)                    (VF forward, utils.py:60-61)
   kReluBwd = 9,   // out = acc * (H > 0), H = the ReLU output    (VF backward)
 };
-// the row-wise softmax heads (one output row per 32-lane wave half)
+// the row-wise softmax heads (one output row per 32-lane wave half, up to kMaxHeadTiles 32-column tiles)
+constexpr int kMaxHeadTiles = 4;
 constexpr bool epi_is_head(int e) { return e >= (int)RowEpi::kPrepHead && e <= (int)RowEpi::kRHead; }
 
 struct RowEpiArgs {

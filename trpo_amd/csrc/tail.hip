@@ -43,11 +43,15 @@ constexpr int SLD = 36;      // row stride (floats) of the [row][action] LDS til
 
 __device__ __forceinline__ float omsq(float h) { return (1.0f - h) * (1.0f + h); }
 
-__device__ __forceinline__ double hsum32(double v) {
+template <class T>
+__device__ __forceinline__ T hsum32t(T v) {
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 32);
   return v;
 }
+#ifndef TRPO_TAIL_HEAD64
+#define TRPO_TAIL_HEAD64 0
+#endif
 
 // the max of a running-max slot (kAmaxSub counters) -> power-of-two scale exponent; whole wave
 __device__ __forceinline__ int slot_exp(const unsigned* amax) {
@@ -79,11 +83,7 @@ __device__ __forceinline__ void split8(const float* x, float s, h8& hi, h8& lo) 
   lo = __builtin_bit_cast(h8, L);
 }
 
-// 1 / x in f64: v_rcp_f64 and one Newton step (the head's values end as f32)
-__device__ __forceinline__ double rcp64(double x) {
-  const double r = __builtin_amdgcn_rcp(x);
-  return r * fma(-x, r, 2.0);
-}
+
 
 // a*b ~= ah bh + ah bl + al bh, smallest terms first
 __device__ __forceinline__ f32x16 mfma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
@@ -109,6 +109,9 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
   __shared__ __attribute__((aligned(16))) unsigned short sX[NW][2 * 2 * 32 * 32];
   __shared__ __attribute__((aligned(16))) float sRD[2][TR][SLD];
   __shared__ __attribute__((aligned(16))) float sD[2][TR][SLD];
+  // f16 planes of the tile's [RD_L ; D_L] (mat 0 / 1) as [row][action], converted once per tile
+  // (4 rows per wave) and read back as A fragments (ds_read_b128) and transposed (tr16)
+  __shared__ __attribute__((aligned(16))) unsigned short sP[2 * 2 * TR * 32];
   __shared__ float sMax[2][NW];
   __shared__ float sBias[NW][64];
   __shared__ float sOut[NW];
@@ -247,7 +250,9 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
     }
     lds_barrier();
 
-    // ---- R-softmax head on this wave's two rows (gemm.hip kRHead) ----
+    // ---- R-softmax head on this wave's two rows (gemm.hip kRHead, same cancellation-free form):
+    //      RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k],
+    //      Rp = p (Rz - <p, Rz>), A = p/(p+eps), B = eps/(p+eps); f32 here (TRPO_TAIL_HEAD64: f64) ----
     float m = 0.0f;
     {
       const int j = lr;
@@ -260,16 +265,21 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
 #pragma unroll
         for (int u = 0; u < NW; ++u) zs += reinterpret_cast<const float*>(sX[u])[i * 64 + lane];
         const float z = zs + cj;
-        const double rz = real ? (double)z : 0.0;
-        const double pd = real ? (double)cP[q] : 0.0;    // rows past the split: P = 0 -> RD = 0
-        const double prz = hsum32(pd * rz);
-        const double Rp = pd * (rz - prz);
-        const double inv = rcp64(pd + (double)kEps);
-        const double Aa = real ? pd * inv : 0.0;
-        const double B = real ? (double)kEps * inv : 0.0;
-        const double spB = hsum32(pd * B);
-        const double sRAB = hsum32(Rp * Aa * B);
-        const double rd = A.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
+#if TRPO_TAIL_HEAD64
+        typedef double T;
+#else
+        typedef float T;
+#endif
+        const T rz = real ? (T)z : T(0);
+        const T pd = real ? (T)cP[q] : T(0);    // rows past the split: P = 0 -> RD = 0
+        const T prz = hsum32t(pd * rz);
+        const T Rp = pd * (rz - prz);
+        const T inv = T(1) / (pd + (T)kEps);
+        const T Aa = real ? pd * inv : T(0);
+        const T B = real ? (T)kEps * inv : T(0);
+        const T spB = hsum32t(pd * B);
+        const T sRAB = hsum32t(Rp * Aa * B);
+        const T rd = (T)A.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
         const float rdf = real ? (float)rd : 0.0f;
         const int row = hrow0 + q;
         sRD[par][row][j] = rdf;
@@ -288,26 +298,37 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
     const int eRD = f16_scale_exp(mt);
     const float sRDf = __builtin_ldexpf(1.0f, eRD);
 
-    // ---- R-backward: RDH = RD_L W^T + D_L V^T, DH = D_L W^T (K = actions); [RD_L | D_L] in A
-    //      layout (lane = row lr, actions 16s + 8lh ..) ----
+    // ---- [RD_L ; D_L] -> f16 planes, rows 4w..4w+3 by wave w; the 16-B chunk c of row r sits at
+    //      c ^ ((r >> 2) & 3) (conflict-free A-fragment reads; tr16 reads of 4 consecutive rows) ----
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    auto pof = [](int mat, int pl, int row, int col) {
+      return ((mat * 2 + pl) * TR + row) * 32 + ((((col >> 3) ^ ((row >> 2) & 3))) << 3) + (col & 7);
+    };
+    {
+      const int row = 4 * w + (lane >> 4), col = 2 * (lane & 15);
+#pragma unroll
+      for (int mat = 0; mat < 2; ++mat) {
+        const float sc = mat == 0 ? sRDf : sDf;
+        const float a = (mat == 0 ? sRD[par][row][col] : sD[par][row][col]) * sc;
+        const float bb = (mat == 0 ? sRD[par][row][col + 1] : sD[par][row][col + 1]) * sc;
+        const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, bb);
+        const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], bb - (float)hp[1]);
+        *reinterpret_cast<fp16x2*>(sP + pof(mat, 0, row, col)) = hp;
+        *reinterpret_cast<fp16x2*>(sP + pof(mat, 1, row, col)) = lp;
+      }
+    }
+    lds_barrier();
+
+    // ---- R-backward: RDH = RD_L W^T + D_L V^T, DH = D_L W^T (K = actions); A fragments: lane =
+    //      row lr, actions 16s + 8lh .. ----
     f32x16 aRW = f32x16{}, aDV = f32x16{}, aDW = f32x16{};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float x[8], y[8];
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(&sRD[par][lr][16 * s + 8 * lh]);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(&sRD[par][lr][16 * s + 8 * lh + 4]);
-      const f32x4 y0 = *reinterpret_cast<const f32x4*>(&sD[par][lr][16 * s + 8 * lh]);
-      const f32x4 y1 = *reinterpret_cast<const f32x4*>(&sD[par][lr][16 * s + 8 * lh + 4]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        x[q] = x0[q];
-        x[4 + q] = x1[q];
-        y[q] = y0[q];
-        y[4 + q] = y1[q];
-      }
-      h8 rh_, rl_, dh_, dl_;
-      split8(x, sRDf, rh_, rl_);
-      split8(y, sDf, dh_, dl_);
+      const int col = 16 * s + 8 * lh;
+      const h8 rh_ = *reinterpret_cast<const h8*>(sP + pof(0, 0, lr, col));
+      const h8 rl_ = *reinterpret_cast<const h8*>(sP + pof(0, 1, lr, col));
+      const h8 dh_ = *reinterpret_cast<const h8*>(sP + pof(1, 0, lr, col));
+      const h8 dl_ = *reinterpret_cast<const h8*>(sP + pof(1, 1, lr, col));
       aRW = mfma3(rh_, rl_, wt[s][0], wt[s][1], aRW);
       aDV = mfma3(dh_, dl_, vt[s][0], vt[s][1], aDV);
       aDW = mfma3(dh_, dl_, wt[s][0], wt[s][1], aDW);
@@ -329,26 +350,32 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
         mxo = fmaxf(mxo, fabsf(o));
       }
     }
-    // ---- weight R-gradient: G += RH^T D_L + H^T RD_L (rows are the MFMA k; D_L / RD_L in C
-    //      layout, lane = action, element j of k-step s = row 16s + 8(j>>2) + 4lh + (j&3)) ----
+    // ---- weight R-gradient: G += RH^T D_L + H^T RD_L (rows are the MFMA k).  B fragments (lane =
+    //      action, element e of k-step s = row 16s + 8(e>>2) + 4lh + (e&3)) by transposed reads of
+    //      the planes: lane 4q+p of a 16-lane group addresses row r0 + q, actions 4p .. 4p+3 ----
     {
+      typedef short s8 __attribute__((ext_vector_type(8)));
+      const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+      auto trb = [&](int mat, int pl, int s2) {
+        s8 v;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int row = 16 * s2 + 4 * (g4 >> 1) + 8 * t + q;
+          const s4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s4*)(sP + pof(mat, pl, row, 16 * (g4 & 1) + 4 * pp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * t + e] = r[e];
+        }
+        return __builtin_bit_cast(h8, v);
+      };
       f32x16 g0 = f32x16{}, g1 = f32x16{};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float x[8], y[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int row = 16 * s + 8 * (j >> 2) + 4 * lh + (j & 3);
-          x[j] = sRD[par][row][lr];
-          y[j] = sD[par][row][lr];
-        }
-        h8 bh, bl, ah, al;
-        split8(y, sDf, bh, bl);
+        h8 ah, al;
         split8(&cRH[8 * s], sRHf, ah, al);
-        g0 = mfma3(ah, al, bh, bl, g0);
-        split8(x, sRDf, bh, bl);
+        g0 = mfma3(ah, al, trb(1, 0, s), trb(1, 1, s), g0);
         split8(&cH[8 * s], sHf, ah, al);
-        g1 = mfma3(ah, al, bh, bl, g1);
+        g1 = mfma3(ah, al, trb(0, 0, s), trb(0, 1, s), g1);
       }
       const float fG0 = __builtin_ldexpf(1.0f, -(eRH + eD)), fG1 = __builtin_ldexpf(1.0f, -(eH + eRD));
 #pragma unroll
