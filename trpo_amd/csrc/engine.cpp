@@ -2143,7 +2143,6 @@ static int* option_slot(const std::string& k) {
   if (k == "split_min_k") return &g_options.split_min_k;
   if (k == "graphs") return &g_options.graphs;
   if (k == "tail") return &g_options.tail;
-  if (k == "stagger") return &g_options.stagger;
   throw ArgError("unknown option " + k);
 }
 

@@ -38,8 +38,7 @@ static int env_int(const char* name, int dflt) {
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
                      env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
-                     env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
-                     env_int("TRPO_STAGGER", 0)};
+                     env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1)};
 
 namespace {
 
@@ -677,10 +676,6 @@ rowgemm3_kernel(const RowGemmArgs args) {
   constexpr int STG = NP * (APL + BPL);
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STG];
   if (args.skip && *args.skip) return;
-  if (args.stagger && blockIdx.x >= 256 && blockIdx.x < 512) {
-    // break the lockstep of two co-resident blocks (one in its epilogue while the other computes)
-    for (int i = 0; i < args.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -1783,17 +1778,6 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
       case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
       case 8: launch_row3_cfg<2, 4, 2, 2, EPI, 4>(a, s); break;      // 128 x 256, 2 blocks / CU
       case 9: launch_row3_cfg<2, 4, 2, 2, EPI, 4, 2>(a, s); break;   // 128 x 256, 2 blocks / CU, 2 in flight
-      case 12: launch_row3_cfg<2, 2, 2, 4, EPI, 2, 2>(a, s); break;  // 128 x 256, 4 waves x 128 acc, 2 blocks / CU
-      case 13: launch_row3_cfg<2, 2, 2, 4, EPI, 2, 1>(a, s); break;  // the same, 1 k-tile in flight
-      case 14: launch_row3_cfg<1, 4, 4, 2, EPI, 2, 2>(a, s); break;  // 128 x 256, 4 waves as 1 x 4 (128 x 64 each)
-      case 16: launch_row3_cfg<2, 2, 4, 4, EPI, 1, 2>(a, s); break;  // 256 x 256, 4 waves x 256 acc (1 wave / SIMD)
-      case 17: launch_row3_cfg<2, 2, 4, 4, EPI, 1, 1>(a, s); break;  // the same, 1 k-tile in flight
-      case 15: {                                                      // 13 with a start stagger
-        RowGemmArgs b = a;
-        b.stagger = g_options.stagger;
-        launch_row3_cfg<2, 2, 2, 4, EPI, 2, 1>(b, s);
-        break;
-      }
       case 11: {                                                      // 256 x 256, LDS-DMA, BK 32 (f16 only)
         bool ok = a.f16 != 0;
         for (int i = 0; i < a.nseg; ++i) ok = ok && a.seg[i].ldk % 32 == 0;
@@ -1908,8 +1892,6 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
       switch (g_options.split_wg) {
         case 2: launch_wg3_cfg<4, 2, 2, 4, 2, 2>(a, s); break;   // 256 x 256, 2 stages
         case 3: launch_wg3_cfg<2, 4, 2, 2, 2, 1>(a, s); break;   // 128 x 256
-        case 4: launch_wg3_cfg<2, 2, 4, 4, 1, 2>(a, s); break;   // 256 x 256, 4 waves x 256 acc
-        case 5: launch_wg3_cfg<2, 2, 4, 4, 1, 1>(a, s); break;
         default: launch_wg3_cfg<4, 2, 2, 4, 2, 1>(a, s); break;  // 256 x 256
       }
     }

@@ -25,7 +25,6 @@ struct Options {
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
   int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
   int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
-  int stagger;     // row GEMM 2-blocks-per-CU configs: start-time stagger of co-resident blocks (experiment)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -108,7 +107,6 @@ struct RowGemmArgs {
   RowEpi epi;
   RowEpiArgs ea;
   int f16 = 0;         // split path: 1 = two scaled f16 planes / 3 products, 0 = three bf16 planes / 6
-  int stagger = 0;     // row_cfg experiments: the first round's second co-resident blocks sleep ~4 us x stagger
 };
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
