@@ -271,18 +271,19 @@ def conjugate_gradient(f_Ax: Callable, b, cg_iters=10, residual_tol=1e-10):
     x = np.zeros_like(b)
     rdotr = r.dot(r)
     it = 0
-    for i in range(cg_iters):
-        z = f_Ax(p)
-        v = rdotr / p.dot(z)
-        x += v * p
-        r -= v * z
-        newrdotr = r.dot(r)
-        mu = newrdotr / rdotr
-        p = r + mu * p
-        rdotr = newrdotr
-        it = i + 1
-        if rdotr < residual_tol:
-            break
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):  # p.z = 0: inf / nan, as numpy gives
+        for i in range(cg_iters):
+            z = f_Ax(p)
+            v = rdotr / p.dot(z)
+            x += v * p
+            r -= v * z
+            newrdotr = r.dot(r)
+            mu = newrdotr / rdotr
+            p = r + mu * p
+            rdotr = newrdotr
+            it = i + 1
+            if rdotr < residual_tol:
+                break
     return x, it
 
 
@@ -297,7 +298,8 @@ def linesearch(f: Callable, x, fullstep, expected_improve_rate):
         newfval = f(xnew)
         actual_improve = fval - newfval
         expected_improve = expected_improve_rate * stepfrac
-        ratio = actual_improve / expected_improve
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = actual_improve / expected_improve
         if ratio > ACCEPT_RATIO and actual_improve > 0:
             return xnew, k
     return x, -1
@@ -399,10 +401,13 @@ def trpo_update(theta_prev, batch: Batch, spec: PolicySpec, dtype=np.float64,
     g = policy_grad(thprev, X, a, adv, old, spec, dtype=dtype)
     stepdir, iters = conjugate_gradient(fvp, -g, cg_iters, residual_tol)
     shs = 0.5 * float(stepdir.dot(fvp(stepdir)))
-    lm = math.sqrt(shs / max_kl)
-    fullstep = (stepdir / dtype(lm)).astype(dtype)
+    with np.errstate(invalid="ignore"):                    # np.sqrt: shs < 0 gives nan, as in the reference
+        lm = float(np.sqrt(np.float64(shs / max_kl)))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        fullstep = (stepdir / dtype(lm)).astype(dtype)
     neggdotstepdir = -g.dot(stepdir)
-    rate = float(neggdotstepdir) / lm
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rate = float(np.float64(neggdotstepdir) / np.float64(lm))
 
     def loss(x):
         return losses(x, X, a, adv, old, spec, dtype=dtype)[0]

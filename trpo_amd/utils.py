@@ -192,27 +192,34 @@ def explained_variance(ypred, y):
 def rollout(env, agent, max_pathlength, n_timesteps):
     """utils.py:18-45 for any gym-style env and an agent with act()/prev_action: whole episodes until
     n_timesteps steps are collected.  (For CartPole-v0 the batched device rollout
-    ``Engine.rollout_cartpole`` does this for many environments at once.)  A path is kept when its
-    episode ends (done) or reaches max_pathlength."""
+    ``Engine.rollout_cartpole`` does this for many environments at once.)
+
+    Reference semantics kept as they are: a path is appended only when its episode ends (``done``)
+    within max_pathlength steps (utils.py:35-43); an episode cut off at max_pathlength is dropped,
+    and the step count then advances by the length of the last appended path (utils.py:44 reads the
+    previous ``path``), or raises UnboundLocalError when no path was appended yet, as the reference
+    does.  With gym's CartPole-v0 (TimeLimit 200 < max_pathlength 1000) every episode ends with done."""
     paths = []
-    steps = 0
-    while steps < n_timesteps:
+    timesteps_sofar = 0
+    while timesteps_sofar < n_timesteps:
         obs, actions, rewards, action_dists = [], [], [], []
         ob = env.reset()
         agent.prev_action *= 0.0
         for _ in range(max_pathlength):
-            action, action_dist, ob_in = agent.act(ob)
-            obs.append(ob_in)
+            action, action_dist, ob = agent.act(ob)
+            obs.append(ob)
             actions.append(action)
             action_dists.append(action_dist)
-            ob, reward, done = env.step(action)[:3]
-            rewards.append(reward)
-            if done:
+            res = env.step(action)
+            ob = res[0]
+            rewards.append(res[1])
+            if res[2]:
+                path = {"obs": np.concatenate(np.expand_dims(obs, 0)), "action_dists": np.concatenate(action_dists),
+                        "rewards": np.array(rewards), "actions": np.array(actions)}
+                paths.append(path)
                 agent.prev_action *= 0.0
                 break
-        paths.append({"obs": np.concatenate(np.expand_dims(obs, 0)), "action_dists": np.concatenate(action_dists),
-                      "rewards": np.array(rewards), "actions": np.array(actions)})
-        steps += len(rewards)
+        timesteps_sofar += len(path["rewards"])   # noqa: F821  (the reference's stale-path read)
     return paths
 
 
