@@ -105,6 +105,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return ab if l == 0 else 2 * ab
     if role == "fvp_rbwd":
         return 2 * ab
+    if role == "fvp_tail":          # fused last layer: R-forward (2ab) + R-backward (2ab) + weight R-gradient (2ab)
+        return 6 * ab
     if role == "fvp_head":          # R-forward (2ab) + R-backward (2ab) + wgrad (2ab) of the last layer
         return 3 * ab
     if role == "fvp_headbwd":       # R-backward (2ab) + wgrad (2ab) of the last layer
@@ -127,6 +129,8 @@ def tag_is_split(tag: str, widths) -> bool:
         return get_option("split_wg") != 0 and b > 128
     if role in ("fvp_head", "fvp_headbwd"):
         return False
+    if role == "fvp_tail":              # tail.hip: always the f16 hi+lo split (3 products)
+        return True
     last = l == len(widths) - 2
     out = a if role in ("bwd", "pg_bwd", "fvp_rbwd") else b
     head = last and role in ("fwd", "ls_fwd", "fvp_rfwd")
@@ -158,6 +162,8 @@ def tag_bytes(tag: str, widths, n: int) -> float:
             cols = 2 * w[l] + 2 * w[l + 1]                  # RH, H ; P ; RD_L out
     elif role == "fvp_rbwd":
         cols = 2 * w[l + 1] + 4 * w[l]                      # RD_l, D_l ; H_l, E, RH_l ; RD_{l-1} out
+    elif role == "fvp_tail":
+        cols = 3 * w[l] + 2 * w[l + 1]                      # RH_l, H_l ; P, D_L ; RD_{l-1} out
     elif role == "fvp_wgrad":
         cols = w[0] + w[1] if l == 0 else 2 * w[l] + 2 * w[l + 1]
     elif role in ("fwd", "ls_fwd"):

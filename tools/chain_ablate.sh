@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../trpo_amd/csrc"
 for b in "$@"; do
   mkdir -p ../../build/abl$b
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -DCHAIN_ABL=$b -x hip -c chain.hip -o ../../build/abl$b/chain.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 ../../build/csrc/gemm.hip.o ../../build/abl$b/chain.o ../../build/csrc/vec.hip.o \
-    ../../build/csrc/scan.hip.o ../../build/csrc/engine.cpp.o -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib \
-    -o ../libtrpo_engine_abl$b.so
+  objs=$(ls ../../build/csrc/*.o | grep -v chain.hip.o)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 $objs ../../build/abl$b/chain.o -shared -L/opt/rocm/lib -lrccl \
+    -Wl,-rpath,/opt/rocm/lib -o ../libtrpo_engine_abl$b.so
 done

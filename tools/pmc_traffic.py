@@ -22,17 +22,15 @@ import statistics
 # (kernel template arguments as rocprofv3 prints them; the last rowgemm3/wgrad3 argument is the
 # plane count: 2 = the default f16 split)
 SPECS = {
-    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 2, 1),
-    "fvp_rbwd_l2": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 2, 0),
     "fvp_rfwd_l0": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 0),
     "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 1),
-    "fvp_rfwd_l2": ("rowgemm_kernel<4, 1, 2, 1, 16, 7, 1>", 1, 0),
+    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 1, 0),
+    "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
     "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 2, 2>",
     "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 2, 2>",
-    "fvp_wgrad_l2": "wgrad_kernel<4, 1, 2, 1, 16, 1>",
 }
 
 
@@ -80,11 +78,13 @@ def main():
         wr = 1024 * statistics.mean(r[2] for r in w)
         res["tags"][tag] = {"kernel": sub, "launches": len(f), "read_bytes": rd, "write_bytes": wr,
                             "traffic_bytes": rd + wr, "pmc_run_ms": statistics.mean(r[3] for r in f)}
+    res["fvp_total_bytes"] = sum(v["traffic_bytes"] for v in res["tags"].values())
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
     for t, v in res["tags"].items():
         print(f"{t:14s} {v['launches']:4d}  read {v['read_bytes'] / 1e9:7.2f} GB  write {v['write_bytes'] / 1e9:6.2f} GB"
               f"  {v['pmc_run_ms']:7.2f} ms")
+    print(f"FVP total {res['fvp_total_bytes'] / 1e9:.1f} GB")
 
 
 if __name__ == "__main__":
