@@ -93,6 +93,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
     """Algorithmic FLOPs of one launch of the kernel behind a profile tag."""
     if tag == "fvp_chain":
         return n * chain_flops_per_row(widths)
+    if tag == "fvp_fused":            # fused.hip: the whole FVP incl. weight R-gradients
+        return n * fvp_flops_per_row(widths)
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0
@@ -117,7 +119,7 @@ def tag_flops(tag: str, widths, n: int) -> float:
 def tag_is_split(tag: str, widths) -> bool:
     """Whether the kernel behind a tag runs on the split-bf16 MFMA path (gemm.hip dispatch rules)."""
     from trpo_amd._lib import get_option
-    if tag == "fvp_chain":
+    if tag in ("fvp_chain", "fvp_fused"):
         return True
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
@@ -138,7 +140,7 @@ def tag_is_split(tag: str, widths) -> bool:
 
 
 def tag_peak(tag: str, widths) -> float:
-    if tag == "fvp_chain":            # chain.hip always runs the exact bf16 hi+mid+lo split (6 products)
+    if tag in ("fvp_chain", "fvp_fused"):   # chain.hip / fused.hip: the exact bf16 hi+mid+lo split (6 products)
         return PEAK_BF16_TFLOPS / 6
     return peak_split_tflops() if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
 
@@ -146,6 +148,10 @@ def tag_peak(tag: str, widths) -> float:
 def tag_bytes(tag: str, widths, n: int) -> float:
     """Algorithmic HBM bytes of one launch: each activation operand read once and each output written
     once (f32, real widths; weights and slabs are O(P) and left out)."""
+    if tag == "fvp_fused":            # X, P, D_{L-1} ; H_l, E_{l-1} per hidden layer ; D_l of the hidden layers
+        L = len(widths) - 1
+        cols = widths[0] + 2 * widths[L] + 2 * sum(widths[1:L]) + sum(widths[2:L])
+        return 4.0 * n * cols
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0

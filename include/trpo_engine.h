@@ -183,7 +183,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
  * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph, all-reduces
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
- * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions).
+ * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions), "fused"
+ * (whole FVP incl. weight gradients in one launch of fused.hip for one or two hidden layers of
+ * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

@@ -284,6 +284,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
+    {"fused": 0}, {"fused": 2},                               # chain + GEMM weight gradients ; 4-wave fused FVP
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -291,7 +292,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain", "split_f16", "split_min_k")}
+                                           "split_wg", "chain", "split_f16", "split_min_k", "fused")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -363,6 +364,43 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
         set_option("chain", saved)
     assert_vec_close(out[1], ref, REL, f"chain Hv {obs} {hidden} {A}")
     assert_vec_close(out[1], out[0], REL, f"chain vs row-GEMM Hv {obs} {hidden} {A}")
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (4, [64], 2, 1000),                # C1 dims (the reference policy)
+    (11, [64, 64], 3, 3001),           # C2 dims, partial last group
+    (128, [64, 64], 18, 2048),         # C3 dims, whole groups
+    (37, [50, 33], 7, 129),            # odd widths, one state past a group
+    (128, [64], 32, 63),               # one hidden layer, A = 32, a single partial group
+    (16, [16, 48], 17, 1),             # one state
+    (128, [64, 64], 18, 100_000),      # many groups per persistent workgroup
+])
+def test_fused_fvp_vs_oracle(gpu_available, obs, hidden, A, n):
+    """The one-launch FVP (fused.hip, both workgroup forms) against the float64 oracle and against
+    the chain + weight-gradient GEMM path it replaces (trpo_inksci.py:56-70)."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + 7)
+    v = np.random.RandomState(n + 8).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
+    saved = get_option("fused")
+    out = {}
+    try:
+        for mode in (1, 2, 0):
+            set_option("fused", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            out[mode] = e.fvp(v, 0.0)
+            out[(mode, "again")] = e.fvp(v, 0.0)
+            e.close()
+    finally:
+        set_option("fused", saved)
+    for mode in (1, 2):
+        assert_vec_close(out[mode], ref, REL, f"fused({mode}) Hv {obs} {hidden} {A} n={n}")
+        assert_vec_close(out[mode], out[0], REL, f"fused({mode}) vs chain Hv {obs} {hidden} {A} n={n}")
+        assert np.array_equal(out[mode], out[(mode, "again")]), "fused FVP is not deterministic"
 
 
 def run_mrank(*extra, nproc=2, timeout=600):

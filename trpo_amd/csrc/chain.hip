@@ -33,7 +33,7 @@
 //  * Epilogue operands (H, E, RH, P) and the second-segment activations (X, H,
 //    D) are read straight into acc layout with per-workgroup buffer
 //    descriptors (out-of-range rows / columns read 0 and drop stores).
-#include "common.h"
+#include "chain_common.h"
 #include "kernels.h"
 
 #include <stdexcept>
@@ -46,40 +46,6 @@
 
 namespace trpo {
 namespace {
-
-typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned short cu16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ unsigned short cb_bits(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
-__device__ __forceinline__ float cb_val(unsigned short b) { return __builtin_bit_cast(float, (unsigned)b << 16); }
-
-// x = hi + mid + lo exactly (each a bf16), as gemm.hip's split3
-__device__ __forceinline__ void csplit(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
-  h = cb_bits(x);
-  const float r1 = x - cb_val(h);
-  m = cb_bits(r1);
-  const float r2 = r1 - cb_val(m);
-  l = cb_bits(r2);
-}
-
-// 16-B chunk position of k-group g in image row o: g ^ chain_hsw(o).  Makes the
-// 16-lane groups of a ds_read_b128 (MI355X_MICROARCH.md, LDS table) hit 16
-// distinct 4-bank sets for 64-B rows.
-__host__ __device__ constexpr int chain_hsw(int o) { return (((o >> 2) & 1) * 2) ^ (((o >> 3) & 1) * 3); }
-
-// MFMA k index kk (0..31) of a chunk -> feature offset within the chunk (acc-layout pairing)
-__host__ __device__ constexpr int chain_perm(int kk) {
-  return (kk & 7) < 4 ? 4 * (kk >> 3) + (kk & 7) : 16 + 4 * (kk >> 3) + (kk & 7) - 4;
-}
-
-__device__ __forceinline__ float c_one_minus_sq(float h) { return (1.0f - h) * (1.0f + h); }
-
-__device__ __forceinline__ double sum4lanes(double v) {   // lanes s, s+16, s+32, s+48
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
-}
 
 // ---------------------------------------------------------------------------
 // weight images: one thread per (chunk, row, k-group) writes 8 k-values x 3 planes
@@ -176,25 +142,7 @@ __global__ void __launch_bounds__(WAVES * 64, OCC) fvp_chain_kernel(const ChainA
     r[3] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, o + 12, 0, 0));
     return r;
   };
-  // B operand (3 planes) from two acc-layout tiles
-  auto mkb = [&](const f32x4& x0, const f32x4& x1, cbf16x8 (&b)[3]) {
-    cu16x8 h, m, l;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      unsigned short hh, mm, ll;
-      csplit(x0[j], hh, mm, ll);
-      h[j] = hh;
-      m[j] = mm;
-      l[j] = ll;
-      csplit(x1[j], hh, mm, ll);
-      h[4 + j] = hh;
-      m[4 + j] = mm;
-      l[4 + j] = ll;
-    }
-    b[0] = __builtin_bit_cast(cbf16x8, h);
-    b[1] = __builtin_bit_cast(cbf16x8, m);
-    b[2] = __builtin_bit_cast(cbf16x8, l);
-  };
+  auto mkb = [&](const f32x4& x0, const f32x4& x1, cbf16x8 (&b)[3]) { chain_mkb(x0, x1, b); };
 
   f32x4 acc[OTM], S[OTM], PF[OTM];   // S: first-segment source (RH_l / RD_l); PF: prefetched epilogue operand
 #pragma unroll

@@ -123,6 +123,9 @@ struct trpo_engine {
   // auto (option 1) takes the chain up to 8 register tiles (hidden widths <= 128), where it
   // beats the per-layer row GEMMs; at 16 tiles its per-128-state weight re-streaming
   // (~2 MB of bf16 planes per workgroup tile) costs more than the fusion saves
+  // whole FVP (R-forward, head, R-backward and weight gradients) in one launch (fused.hip): one or
+  // two hidden layers of width <= 64, obs <= 128, <= 32 actions; reuses the chain's weight images
+  bool use_fused() const { return g_options.fused != 0 && chain_otm > 0 && fused_fvp_eligible(L, w.data()); }
   bool use_chain() const {
     return chain_otm > 0 && (g_options.chain >= 2 || (g_options.chain == 1 && chain_otm <= 8));
   }
@@ -850,6 +853,10 @@ struct trpo_engine {
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
   void fvp(const float* v, float* out, const int* skip) {
     prepare();
+    if (use_fused()) {
+      fvp_fused(v, out, skip);
+      return;
+    }
     if (use_chain()) {
       fvp_chain(v, out, skip);
       return;
@@ -1054,19 +1061,7 @@ struct trpo_engine {
     reduce_grad(out, skip);
   }
 
-  // the same Hv with the row-local part (R-forward, R-head, R-backward) in one fused launch
-  void fvp_chain(const float* v, float* out, const int* skip) {
-    if (!chain_w_valid) {
-      Scope sp(this, "fvp_img_w");
-      launch_chain_img(chain_jobs, theta, v, 0, nullptr, stream);
-      check_launch();
-      chain_w_valid = true;
-    }
-    {
-      Scope sp(this, "fvp_img_v");
-      launch_chain_img(chain_jobs, theta, v, 1, skip, stream);
-      check_launch();
-    }
+  ChainArgs chain_args(const float* v, const int* skip) const {
     ChainArgs ca{};
     ca.n = (int)n;
     ca.L = L;
@@ -1090,6 +1085,60 @@ struct trpo_engine {
     ca.nchunks = chain_nchunks;
     ca.invN = 1.0 / (double)n_global;
     ca.skip = skip;
+    return ca;
+  }
+
+  // the whole Hv in one launch (fused.hip) + the slab reduction
+  void fvp_fused(const float* v, float* out, const int* skip) {
+    if (!chain_w_valid) {
+      Scope sp(this, "fvp_img_w");
+      launch_chain_img(chain_jobs, theta, v, 0, nullptr, stream);
+      check_launch();
+      chain_w_valid = true;
+    }
+    {
+      Scope sp(this, "fvp_img_v");
+      launch_chain_img(chain_jobs, theta, v, 1, skip, stream);
+      check_launch();
+    }
+    const int variant = g_options.fused == 2 ? 2 : 1;
+    const int rb = fused_fvp_states_per_group(variant);
+    FusedArgs fa{};
+    fa.c = chain_args(v, skip);
+    fa.slab = slab;
+    fa.slab_stride = slab_stride;
+    for (int l = 0; l < L; ++l) fa.offW[l] = offW[l];
+    fa.ngroups = (int)((n + rb - 1) / rb);
+    // one persistent workgroup per CU (8 waves) or two (4 waves), at most one per slab
+    const int per_cu = variant == 2 ? 2 : 1;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)fa.ngroups, (int64_t)S, (int64_t)256 * per_cu}));
+    {
+      Scope sp(this, "fvp_fused");
+      launch_fvp_fused(fa, grid, variant, stream);
+      check_launch();
+    }
+    {
+      Scope sp(this, "reduce");
+      launch_reduce_slab(slab, grid, slab_stride, P, out, skip, stream);
+      check_launch();
+    }
+    allreduce_f32(out, (size_t)P);
+  }
+
+  // the same Hv with the row-local part (R-forward, R-head, R-backward) in one fused launch
+  void fvp_chain(const float* v, float* out, const int* skip) {
+    if (!chain_w_valid) {
+      Scope sp(this, "fvp_img_w");
+      launch_chain_img(chain_jobs, theta, v, 0, nullptr, stream);
+      check_launch();
+      chain_w_valid = true;
+    }
+    {
+      Scope sp(this, "fvp_img_v");
+      launch_chain_img(chain_jobs, theta, v, 1, skip, stream);
+      check_launch();
+    }
+    const ChainArgs ca = chain_args(v, skip);
     {
       Scope sp(this, "fvp_chain");
       launch_fvp_chain(ca, chain_otm, stream);
@@ -2143,6 +2192,7 @@ static int* option_slot(const std::string& k) {
   if (k == "split_min_k") return &g_options.split_min_k;
   if (k == "graphs") return &g_options.graphs;
   if (k == "tail") return &g_options.tail;
+  if (k == "fused") return &g_options.fused;
   throw ArgError("unknown option " + k);
 }
 

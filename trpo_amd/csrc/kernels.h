@@ -25,6 +25,7 @@ struct Options {
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
   int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
   int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
+  int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -378,6 +379,24 @@ int chain_max_tiles(int max_hidden);   // register tiles for a max hidden width 
 void launch_fvp_chain(const ChainArgs& a, int otm, hipStream_t s);
 void launch_chain_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
                       hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Fused small-width FVP (fused.hip): the chain above plus the weight R-gradients in one
+// persistent launch, for one or two hidden layers of width <= 64, obs <= 128, <= 32 actions.
+// Reads the chain's ChainArgs (the RH / RD pointers are not used) and writes one partial Hv per
+// workgroup to slab[blockIdx.x] (all P entries); launch_reduce_slab over `grid` slabs finishes it.
+// variant 1: 8 waves, 128 states per group (one workgroup per CU); 2: 4 waves, 64 states.
+// ---------------------------------------------------------------------------
+struct FusedArgs {
+  ChainArgs c;
+  float* slab;
+  int64_t slab_stride;
+  int64_t offW[kMaxLayers];
+  int ngroups;                       // ceil(n / states per group)
+};
+bool fused_fvp_eligible(int L, const int* w);
+int fused_fvp_states_per_group(int variant);
+void launch_fvp_fused(const FusedArgs& a, int grid, int variant, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
