@@ -30,6 +30,12 @@
 
 #include <stdexcept>
 
+// Ablation build for profiling only (tools/fused_ablate.sh; never the shipped library): bit 0 = no
+// per-state activation loads, bit 1 = no weight-gradient passes, bit 2 = no weight-chunk staging.
+#ifndef FUSED_ABL
+#define FUSED_ABL 0
+#endif
+
 namespace trpo {
 namespace {
 
@@ -54,13 +60,9 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
   constexpr int PL = RB * kFI;                // u16 per image plane
   constexpr int KS = RB / 32;                 // k-steps of a gradient pass
   constexpr int RING = 2;
-#ifdef ABL_TW1
-  constexpr int TW0 = 1, TWH = 1, TWL = 1;
-#else
   constexpr int TW0 = (OBC * 16 + FW - 1) / FW;   // owned tiles: obs x hidden
   constexpr int TWH = (16 + FW - 1) / FW;         //              hidden x hidden (NL == 3)
   constexpr int TWL = (8 + FW - 1) / FW;          //              hidden x actions
-#endif
   __shared__ cu32x4 wl[CHU];
   __shared__ __attribute__((aligned(16))) unsigned short simg[2][3 * PL];   // [act | delta] images
   __shared__ float sb[FW][NL][64];                                         // per-wave bias sums
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
       qq = qq < a.nchunks ? qq : a.nchunks - 1;
       const int off = a.tab[2 * qq], sz = a.tab[2 * qq + 1];
       const cu32x4* src = img + off;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < NLD; ++i) {
         const int idx = tid + i * NT;
         wr[i] = src[idx < sz ? idx : sz - 1];
@@ -115,20 +117,22 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     auto chunk_begin = [&]() __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
       lds_barrier();   // every wave is done with the previous chunk (and with the previous pass)
-  #pragma unroll
-      for (int i = 0; i < NLD; ++i) {
-        const int idx = tid + i * NT;
-        if (CHU % NT == 0 || idx < CHU) wl[idx] = wr[i];
+      if constexpr ((FUSED_ABL & 4) == 0) {
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+          const int idx = tid + i * NT;
+          if (CHU % NT == 0 || idx < CHU) wl[idx] = wr[i];
+        }
       }
       lds_barrier();
-      gload(++q);
+      if constexpr ((FUSED_ABL & 4) == 0) gload(++q);
     };
 
     // ---- image helpers ----
     // acc-layout tile t of this lane (features 16t + 4g.., state lrow) -> 3 planes
     auto put4 = [&](unsigned short* slot, int t, const f32x4& x) {
       cu16x4 h, m, l;
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 4; ++j) {
         unsigned short hh, mm, ll;
         csplit(x[j], hh, mm, ll);
@@ -144,7 +148,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     // chain B operand of chunk c (tiles 2c, 2c+1) -> 3 planes
     auto putb = [&](unsigned short* slot, int c, const cbf16x8 (&b)[3]) {
       const int o0 = fimg(lrow, 32 * c + 4 * g), o1 = fimg(lrow, 32 * c + 16 + 4 * g);
-  #pragma unroll
+#pragma unroll
       for (int p = 0; p < 3; ++p) {
         const cu16x8 v = __builtin_bit_cast(cu16x8, b[p]);
         *reinterpret_cast<cu16x4*>(slot + p * PL + o0) = cu16x4{v[0], v[1], v[2], v[3]};
@@ -154,15 +158,15 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     // 16x16x32 operand of feature tile ft, k-step ks: lane (i = lane&15, g) <- states 32ks + 8g .. +7
     const int tq = (lane >> 2) & 3, tp = lane & 3;
     auto tfrag = [&](const unsigned short* slot, int ft, int ks, cbf16x8 (&f)[3]) {
-  #pragma unroll
+#pragma unroll
       for (int p = 0; p < 3; ++p) {
         fs8 v;
-  #pragma unroll
+#pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int r = 32 * ks + 8 * g + 4 * t + tq;
           const fs4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) fs4*)(slot + p * PL + r * kFI + (((ft ^ fswz(r))) << 4) + 4 * tp));
-  #pragma unroll
+#pragma unroll
           for (int e = 0; e < 4; ++e) v[4 * t + e] = x[e];
         }
         f[p] = __builtin_bit_cast(cbf16x8, v);
@@ -172,13 +176,13 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     // [ti0, ti0 + 4) against the two images
     auto run = [&](auto& dacc, int TI, int TJ, int ti0) __attribute__((always_inline)) {
       constexpr int TWm = sizeof(dacc) / sizeof(f32x4);
-  #pragma unroll
+#pragma unroll
       for (int k = 0; k < TWm; ++k) {
         const int u = wave + FW * k;
         const int it = u / TJ, jt = u - (u / TJ) * TJ;
         if (u < TI * TJ && it >= ti0 && it < ti0 + 4) {
           f32x4 c = dacc[k];
-  #pragma unroll
+#pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             cbf16x8 fa_[3], fd_[3];
             tfrag(sA, it - ti0, ks, fa_);
@@ -192,11 +196,11 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     };
     // bias sums of layer m from acc-layout RD tiles: sum over the wave's 16 states
     auto bias_add = [&](int m, int OT, const f32x4 (&R)[OTM]) {
-  #pragma unroll
+#pragma unroll
       for (int t = 0; t < OTM; ++t) {
         if (t < OT) {
           f32x4 v = R[t];
-  #pragma unroll
+#pragma unroll
           for (int j = 0; j < 4; ++j) {
             float x = v[j];
             x += __shfl_xor(x, 1, 16);
@@ -206,7 +210,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
             v[j] = x;
           }
           if (s == 0) {
-  #pragma unroll
+#pragma unroll
             for (int j = 0; j < 4; ++j) sb[wave][m][16 * t + 4 * g + j] += v[j];
           }
         }
@@ -222,6 +226,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
       return col < ld ? (lrow * ld + col) * 4 : rb * ld * 4;
     };
     auto ld4 = [&](__amdgpu_buffer_rsrc_t r, int vo) -> f32x4 {
+      if constexpr (FUSED_ABL & 1) return f32x4{0.5f, 0.25f, 0.125f, 0.0625f};
       return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0));
     };
     auto bias4 = [&](int l, int t) -> f32x4 {
@@ -339,6 +344,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
 
     // a gradient pass of layer m with the act image holding act tiles [ti0, ti0+4)
     auto pass_run = [&](int m, int ti0) __attribute__((always_inline)) {
+      if constexpr ((FUSED_ABL & 2) != 0) return;
       __builtin_amdgcn_sched_barrier(0);
       const int TI = (a.w[m] + 15) >> 4, TJ = (a.w[m + 1] + 15) >> 4;
       if (m == 0) run(dw0, TI, TJ, ti0);
@@ -365,11 +371,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
           for (int i = 0; i < 4; ++i) r[i] = c_one_minus_sq(h[i]) * (acc[t][i] + cb[i]);
         }
         S[t] = r;
-#ifdef ABL_RHMEM
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(cu32x4, r), rsrc(a.RH[j], ldj), voff(ldj, t), 0, 0);
-#else
         RHk[j][t] = r;
-#endif
       }
     }
 
@@ -448,12 +450,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
         f32x4 r = z4;
         if (t < OT) {
           const int vo = voff(ldl, t);
-#ifdef ABL_RHMEM
-          const f32x4 h = ld4(rH, vo), e = PF[t], rh = ld4(rsrc(a.RH[l], ldl), vo);
-          RHk[l][t] = rh;
-#else
           const f32x4 h = ld4(rH, vo), e = PF[t], rh = RHk[l][t];
-#endif
 #pragma unroll
           for (int i = 0; i < 4; ++i) r[i] = fmaf(e[i], rh[i], acc[t][i] * c_one_minus_sq(h[i]));
         }

@@ -37,7 +37,7 @@ static int env_int(const char* name, int dflt) {
 }
 Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_int("TRPO_FUSED_HEAD", 0),
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
-                     env_int("TRPO_SPLIT_WG", 2), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
+                     env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
                      env_int("TRPO_FUSED", 1)};
 
@@ -842,7 +842,12 @@ rowgemm3_kernel(const RowGemmArgs args) {
   // product scale (powers of two: exact)
   auto seg_switch = [&](int t) {
     if constexpr (NP == 2) {
-      if (t == nt0 && nt1 > 0) scale_acc<TM, TN>(acc, eP1 - eP0);
+      if (t == nt0 && nt1 > 0) {
+        // a real branch: the volatile asm keeps the compiler from if-converting the rescale into
+        // an unconditional multiply of every accumulator on every k-tile
+        asm volatile("; segment switch" ::: "memory");
+        scale_acc<TM, TN>(acc, eP1 - eP0);
+      }
     }
   };
 
@@ -937,58 +942,67 @@ wgrad3_kernel(const WGradArgs args) {
   float csum[BP];
 #pragma unroll
   for (int i = 0; i < BP; ++i) csum[i] = 0.0f;
+  // Per-split buffer descriptors over rows [r0, r1) of each segment operand: rows past r1 read 0 and a
+  // lane whose column is out of range addresses past the end (reads 0), so a load is one buffer op with
+  // a lane-constant voffset and a scalar row offset -- no per-load 64-bit address math or selects.
+  auto desc = [&](const float* p, int ld) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (size_t)r0 * ld), 0, (r1 - r0) * ld * 4, 0x00020000);
+  };
+  const int lda4 = args.seg[0].lda * 4, ldb4 = args.seg[0].ldb * 4;   // equal across segments (host check)
+  constexpr int kOob = 0x40000000;
+  int vA[AP], vB[BP];
+#pragma unroll
+  for (int i = 0; i < AP; ++i) {
+    const int f = tid + i * NT;
+    const int c = f % BM, g = f / BM;
+    const bool okc = (AI % NT == 0 || f < AI) && m0 + c < args.Mpad;
+    vA[i] = okc ? 8 * g * lda4 + (m0 + c) * 4 : kOob;
+  }
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int f = tid + i * NT;
+    const int c = f % BN, g = f / BN;
+    const bool okc = (BI % NT == 0 || f < BI) && n0 + c < args.Npad;
+    vB[i] = okc ? 8 * g * ldb4 + (n0 + c) * 4 : kOob;
+  }
+  auto ldbuf = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  };
   struct Stage {
     float va[AP][8], vb[BP][8];
-    int nv;          // valid rows of the tile (>= 16: all)
     bool cs;         // this tile belongs to the column-summed segment
     int sg;          // segment
   };
   auto gload = [&](Stage& st, int t) {
     const int sg = t / nk;
     const int kt = t - sg * nk;
-    const float* Ap = sg ? args.seg[1].A : args.seg[0].A;
-    const float* Bp = sg ? args.seg[1].B : args.seg[0].B;
-    const int lda = sg ? args.seg[1].lda : args.seg[0].lda;
-    const int ldb = sg ? args.seg[1].ldb : args.seg[0].ldb;
-    const int rb0 = r0 + kt * BK;
-    st.nv = r1 - rb0;
     st.cs = do_colsum && sg == args.colsum_seg;
     st.sg = sg;
+    // descriptors from the (wave-uniform) segment's pointers, built here: a select between two
+    // prebuilt descriptors came out in VGPRs and put every load in a readfirstlane loop
+    const __amdgpu_buffer_rsrc_t ra = desc(sg ? args.seg[1].A : args.seg[0].A, args.seg[0].lda);
+    const __amdgpu_buffer_rsrc_t rb = desc(sg ? args.seg[1].B : args.seg[0].B, args.seg[0].ldb);
+    const int sa = kt * BK * lda4, sb = kt * BK * ldb4;
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < AP; ++i) {
-      const int f = tid + i * NT;
-      const int c = f % BM, g = f / BM;
-      const bool okc = (AI % NT == 0 || f < AI) && m0 + c < args.Mpad;
+    for (int i = 0; i < AP; ++i)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = rb0 + 8 * g + q;
-        const bool ok = okc && r < r1;
-        st.va[i][q] = Ap[(size_t)(ok ? r : r0) * lda + (ok ? m0 + c : 0)];
-      }
-    }
+      for (int q = 0; q < 8; ++q) st.va[i][q] = ldbuf(ra, vA[i], sa + q * lda4);
 #pragma unroll
-    for (int i = 0; i < BP; ++i) {
-      const int f = tid + i * NT;
-      const int c = f % BN, g = f / BN;
-      const bool okc = (BI % NT == 0 || f < BI) && n0 + c < args.Npad;
+    for (int i = 0; i < BP; ++i)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = rb0 + 8 * g + q;
-        const bool ok = okc && r < r1;
-        st.vb[i][q] = Bp[(size_t)(ok ? r : r0) * ldb + (ok ? n0 + c : 0)];
-      }
-    }
+      for (int q = 0; q < 8; ++q) st.vb[i][q] = ldbuf(rb, vB[i], sb + q * ldb4);
+    __builtin_amdgcn_sched_barrier(0);
   };
-  auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int nv, int e) {
+  auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int e) {
     unsigned short* dst = base + swz16(c, g);
     if constexpr (NP == 2) {
       const float sc = __builtin_ldexpf(1.0f, e);
       u16x8 h, l;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float x = (8 * g + q < nv) ? v[q] : 0.0f;
         unsigned short hh, ll;
-        split2h(x * sc, hh, ll);
+        split2h(v[q] * sc, hh, ll);
         h[q] = hh;
         l[q] = ll;
       }
@@ -998,9 +1012,8 @@ wgrad3_kernel(const WGradArgs args) {
       u16x8 h, m, l;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float x = (8 * g + q < nv) ? v[q] : 0.0f;
         unsigned short hh, mm, ll;
-        split3(x, hh, mm, ll);
+        split3(v[q], hh, mm, ll);
         h[q] = hh;
         m[q] = mm;
         l[q] = ll;
@@ -1016,23 +1029,17 @@ wgrad3_kernel(const WGradArgs args) {
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
-      if (AI % NT == 0 || f < AI) {
-        const int c = f % BM, g = f / BM;
-        // an invalid column holds finite clamped data; zero it through nv = 0
-        put(As, APL, c, g, st.va[i], m0 + c < args.Mpad ? st.nv : 0, eA[st.sg]);
-      }
+      if (AI % NT == 0 || f < AI) put(As, APL, f % BM, f / BM, st.va[i], eA[st.sg]);
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
       const int f = tid + i * NT;
       if (BI % NT == 0 || f < BI) {
-        const int c = f % BN, g = f / BN;
-        const int nv = n0 + c < args.Npad ? st.nv : 0;
-        put(Bs, BPL, c, g, st.vb[i], nv, eB[st.sg]);
+        put(Bs, BPL, f % BN, f / BN, st.vb[i], eB[st.sg]);
         if (st.cs) {
           float cs = 0.0f;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) cs += (8 * g + q < nv) ? st.vb[i][q] : 0.0f;
+          for (int q = 0; q < 8; ++q) cs += st.vb[i][q];
           csum[i] += cs;
         }
       }
@@ -1084,7 +1091,10 @@ wgrad3_kernel(const WGradArgs args) {
   };
   auto seg_switch = [&](int t) {
     if constexpr (NP == 2) {
-      if (t == nk && args.nseg > 1) scale_acc<TM, TN>(acc, (eA[1] + eB[1]) - (eA[0] + eB[0]));
+      if (t == nk && args.nseg > 1) {
+        asm volatile("; segment switch" ::: "memory");   // a real branch (see rowgemm3_kernel)
+        scale_acc<TM, TN>(acc, (eA[1] + eB[1]) - (eA[0] + eB[0]));
+      }
     }
   };
 
@@ -1779,6 +1789,8 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
       case 7: launch_row3_cfg<4, 4, 2, 2, EPI, 4>(a, s); break;      // 256 x 256, 16 waves
       case 8: launch_row3_cfg<2, 4, 2, 2, EPI, 4>(a, s); break;      // 128 x 256, 2 blocks / CU
       case 9: launch_row3_cfg<2, 4, 2, 2, EPI, 4, 2>(a, s); break;   // 128 x 256, 2 blocks / CU, 2 in flight
+      case 12: launch_row3_cfg<2, 2, 2, 4, EPI, 2, 2>(a, s); break;  // 128 x 256, 4 waves, 2 blocks / CU
+      case 13: launch_row3_cfg<2, 2, 2, 4, EPI, 2, 1>(a, s); break;  // the same, one k-tile in flight
       case 11: {                                                      // 256 x 256, LDS-DMA, BK 32 (f16 only)
         bool ok = a.f16 != 0;
         for (int i = 0; i < a.nseg; ++i) ok = ok && a.seg[i].ldk % 32 == 0;
@@ -1828,6 +1840,10 @@ template <int WM, int WN, int TM, int TN, int OCC, int PF>
 void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   if (a.rows_per_split % 16) throw std::runtime_error("split-bf16 wgrad: rows_per_split % 16");
+  if (a.nseg > 1 && (a.seg[1].lda != a.seg[0].lda || a.seg[1].ldb != a.seg[0].ldb))
+    throw std::runtime_error("split-bf16 wgrad: segments with different leading dimensions");
+  if ((int64_t)a.rows_per_split * (a.seg[0].lda > a.seg[0].ldb ? a.seg[0].lda : a.seg[0].ldb) * 4 >= (int64_t(1) << 30))
+    throw std::runtime_error("split-bf16 wgrad: a split's rows exceed the 1 GiB buffer-descriptor range");
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
   if (a.f16)
     hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 2>), grid, dim3(WM * WN * 64), 0, s, a);
@@ -1892,6 +1908,8 @@ void launch_wgrad(const WGradArgs& a, hipStream_t s) {
     } else {
       switch (g_options.split_wg) {
         case 2: launch_wg3_cfg<4, 2, 2, 4, 2, 2>(a, s); break;   // 256 x 256, 2 stages
+        case 4: launch_wg3_cfg<2, 2, 2, 4, 2, 2>(a, s); break;   // 128 x 256, 4 waves, 2 blocks / CU
+        case 5: launch_wg3_cfg<2, 2, 4, 2, 2, 2>(a, s); break;   // 256 x 128, 4 waves, 2 blocks / CU
         case 3: launch_wg3_cfg<2, 4, 2, 2, 2, 1>(a, s); break;   // 128 x 256
         default: launch_wg3_cfg<4, 2, 2, 4, 2, 1>(a, s); break;  // 256 x 256
       }
