@@ -185,7 +185,7 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
  * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions), "fused"
  * (whole FVP incl. weight gradients in one launch of fused.hip for one or two hidden layers of
- * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups).
+ * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups, the default).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

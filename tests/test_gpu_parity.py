@@ -284,7 +284,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
-    {"fused": 0}, {"fused": 2},                               # chain + GEMM weight gradients ; 4-wave fused FVP
+    {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and

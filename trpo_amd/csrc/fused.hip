@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
   __shared__ cu32x4 wl[CHU];
   __shared__ __attribute__((aligned(16))) unsigned short simg[2][3 * PL];   // [act | delta] images
   __shared__ float sb[FW][NL][64];                                         // per-wave bias sums
+  __shared__ __attribute__((aligned(16))) float sc[NL][64];               // the tangent's biases c_l
 
   const ChainArgs& a = fa.c;
   if (a.skip && *a.skip) return;
@@ -78,6 +79,10 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
   unsigned short* const sD = &simg[1][0];
 
   for (int i = tid; i < FW * NL * 64; i += NT) (&sb[0][0][0])[i] = 0.0f;
+  for (int i = tid; i < NL * 64; i += NT) {   // read once: every step's epilogue adds them
+    const int l = i >> 6, j = i & 63;
+    sc[l][j] = j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
+  }
 
   f32x4 dw0[TW0], dwh[TWH], dwl[TWL];
 #pragma unroll
@@ -88,6 +93,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
   for (int k = 0; k < TWL; ++k) dwl[k] = z4;
 
   f32x4 acc[OTM], S[OTM], PF[OTM], RHk[NL][OTM];
+  f32x4 xn0 = z4, xn1 = z4;   // first X chunk of the next group (loaded one group ahead)
   const int ngroups = fa.ngroups;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t row_b = (int64_t)grp * RB;
@@ -144,6 +150,17 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
       *reinterpret_cast<cu16x4*>(slot + o) = h;
       *reinterpret_cast<cu16x4*>(slot + PL + o) = m;
       *reinterpret_cast<cu16x4*>(slot + 2 * PL + o) = l;
+    };
+    // the f32 values of acc-layout tile t of this lane back from the 3 planes (exact: hi + mid + lo)
+    auto get4 = [&](const unsigned short* slot, int t) -> f32x4 {
+      const int o = fimg(lrow, 16 * t + 4 * g);
+      const cu16x4 h = *reinterpret_cast<const cu16x4*>(slot + o);
+      const cu16x4 m = *reinterpret_cast<const cu16x4*>(slot + PL + o);
+      const cu16x4 l = *reinterpret_cast<const cu16x4*>(slot + 2 * PL + o);
+      f32x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = (cb_val(h[j]) + cb_val(m[j])) + cb_val(l[j]);
+      return r;
     };
     // chain B operand of chunk c (tiles 2c, 2c+1) -> 3 planes
     auto putb = [&](unsigned short* slot, int c, const cbf16x8 (&b)[3]) {
@@ -229,17 +246,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
       if constexpr (FUSED_ABL & 1) return f32x4{0.5f, 0.25f, 0.125f, 0.0625f};
       return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0));
     };
-    auto bias4 = [&](int l, int t) -> f32x4 {
-      const __amdgpu_buffer_rsrc_t rc =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(a.v + a.offb[l]), 0, a.w[l + 1] * 4, 0x00020000);
-      const int o = (16 * t + 4 * g) * 4;
-      f32x4 r;
-      r[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, o, 0, 0));
-      r[1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, o + 4, 0, 0));
-      r[2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, o + 8, 0, 0));
-      r[3] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, o + 12, 0, 0));
-      return r;
-    };
+    auto bias4 = [&](int l, int t) -> f32x4 { return *reinterpret_cast<const f32x4*>(&sc[l][16 * t + 4 * g]); };
 
     auto mma_tile = [&](const unsigned short* W, int pl, int ot, const cbf16x8 (&b)[3]) __attribute__((always_inline)) {
       cbf16x8 w3[3];
@@ -283,7 +290,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     // One chain step: acc = [S (kc0 chunks, registers) | M1 (kc1 chunks, memory)] x images, with
     // the epilogue operand Pre prefetched into PF; cap (optional) receives M1's split planes.
     auto step = [&](int OT, int kc0, const float* M1, int ld1, int kc1, const float* Pre, int ldp, int OTp,
-                    unsigned short* cap) __attribute__((always_inline)) {
+                    unsigned short* cap, bool pre = false) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);   // keep each step's loads inside the step
 #pragma unroll
       for (int t = 0; t < OTM; ++t) acc[t] = z4;
@@ -291,7 +298,10 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
       const int oob1 = rb * ld1 * 4;
       auto mld = [&](int cc, int h) { return ld4(r1, cc < kc1 ? voff(ld1, 2 * cc + h) : oob1); };
       f32x4 n0 = z4, n1 = z4, m0 = z4, m1 = z4;
-      if (kc0 < RING) {
+      if (pre) {            // the first chunk was loaded ahead (X of this group, issued by the previous one)
+        n0 = xn0;
+        n1 = xn1;
+      } else if (kc0 < RING) {
         n0 = mld(0, 0);
         n1 = mld(0, 1);
       }
@@ -354,12 +364,17 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
 
     q = 0;
     gload(0);
+    if (grp == (int)blockIdx.x) {   // later groups' first X chunk is loaded during the previous group
+      const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
+      xn0 = ld4(rx, voff(a.ld[0], 0));
+      xn1 = ld4(rx, voff(a.ld[0], 1));
+    }
 
     // ---- R-forward through the hidden layers: RH_{l+1} = (1 - H^2)(RH_l W + H_l V + c) ----
 #pragma unroll
     for (int l = 0; l < NL - 1; ++l) {
       const int j = l + 1, OT = (a.w[j] + 15) >> 4, kc = (a.w[l] + 31) >> 5, ldj = a.ld[j];
-      if (l == 0) step(OT, 0, a.X, a.ld[0], kc, a.H[j], ldj, OT, nullptr);
+      if (l == 0) step(OT, 0, a.X, a.ld[0], kc, a.H[j], ldj, OT, nullptr, true);
       else step(OT, kc, a.H[l], a.ld[l], kc, a.H[j], ldj, OT, nullptr);
 #pragma unroll
       for (int t = 0; t < OTM; ++t) {
@@ -444,22 +459,31 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
     for (int l = NL - 1; l >= 1; --l) {
       const int OT = (a.w[l] + 15) >> 4, kc = (a.w[l + 1] + 31) >> 5, ldl = a.ld[l];
       step(OT, kc, a.D[l], a.ld[l + 1], kc, a.E[l - 1], ldl, OT, sD);
-      const __amdgpu_buffer_rsrc_t rH = rsrc(a.H[l], ldl);
+      // H_l for (1 - H_l^2) comes from the act image, which holds this wave's own rows of H_l at this
+      // point (captured in the head step for l = NL-1, re-read for the previous pass otherwise): the
+      // three bf16 planes sum back to the f32 value exactly, and no HBM load sits on the critical path
 #pragma unroll
       for (int t = 0; t < OTM; ++t) {
         f32x4 r = z4;
         if (t < OT) {
-          const int vo = voff(ldl, t);
-          const f32x4 h = ld4(rH, vo), e = PF[t], rh = RHk[l][t];
+          const f32x4 h = get4(sA, t), e = PF[t], rh = RHk[l][t];
 #pragma unroll
           for (int i = 0; i < 4; ++i) r[i] = fmaf(e[i], rh[i], acc[t][i] * c_one_minus_sq(h[i]));
         }
         S[t] = r;
       }
-      // (Hv)_W_l += RH_l^T D_l
+      // (Hv)_W_l += RH_l^T D_l ; the next pass's act operand (H_{l-1}, or X's first 64 features) is
+      // loaded meanwhile
       lds_barrier();
 #pragma unroll
       for (int t = 0; t < OTM; ++t) put4(sA, t, RHk[l][t]);
+      f32x4 nxt[OTM];
+      {
+        const int ldn = a.ld[l - 1];
+        const __amdgpu_buffer_rsrc_t rn = rsrc(l - 1 >= 1 ? a.H[l - 1] : a.X, ldn);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rn, voff(ldn, t));
+      }
       lds_barrier();
       pass_run(l, 0);
       // (Hv)_W_{l-1} += H_{l-1}^T RD_{l-1}  (X for l-1 = 0, in 64-feature chunks)
@@ -467,21 +491,34 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
 #pragma unroll
       for (int t = 0; t < OTM; ++t) put4(sD, t, S[t]);
       bias_add(l - 1, OT, S);
-      if (l - 1 >= 1) {
-        const __amdgpu_buffer_rsrc_t rh = rsrc(a.H[l - 1], a.ld[l - 1]);
 #pragma unroll
-        for (int t = 0; t < OTM; ++t) put4(sA, t, ld4(rh, voff(a.ld[l - 1], t)));
+      for (int t = 0; t < OTM; ++t) put4(sA, t, nxt[t]);
+      if (l - 1 >= 1) {
         lds_barrier();
         pass_run(l - 1, 0);
       } else {
         const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
 #pragma unroll
         for (int ch = 0; ch < OBC; ++ch) {
-          if (ch > 0) lds_barrier();
+          if (ch + 1 < OBC) {
 #pragma unroll
-          for (int t = 0; t < OTM; ++t) put4(sA, t, ld4(rx, voff(a.ld[0], 4 * ch + t)));
+            for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], 4 * (ch + 1) + t));
+          } else {
+            // the next group's first X chunk, in flight during this last gradient pass
+            const int64_t nb = row_b + (int64_t)gridDim.x * RB;
+            const int nrb = (int)((int64_t)a.n - nb < RB ? (int64_t)a.n - nb : RB);
+            const __amdgpu_buffer_rsrc_t rxn = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(a.X + (nb < a.n ? nb : 0) * a.ld[0]), 0, nb < a.n ? nrb * a.ld[0] * 4 : 0, 0x00020000);
+            xn0 = ld4(rxn, voff(a.ld[0], 0));
+            xn1 = ld4(rxn, voff(a.ld[0], 1));
+          }
           lds_barrier();
           pass_run(0, 4 * ch);
+          if (ch + 1 < OBC) {
+            lds_barrier();
+#pragma unroll
+            for (int t = 0; t < OTM; ++t) put4(sA, t, nxt[t]);
+          }
         }
       }
     }

@@ -25,7 +25,7 @@ struct Options {
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
   int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
   int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
-  int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves
+  int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves (default)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
