@@ -350,9 +350,10 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
     dd = O.synthetic_batch(spec, n, seed=n)
     v = np.random.RandomState(n + 1).standard_normal(spec.n_params).astype(np.float32)
     ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], v.astype(np.float64), spec)
-    saved = get_option("chain")
+    saved = get_option("chain"), get_option("fused")
     out = {}
     try:
+        set_option("fused", 0)     # the chain itself, also where the one-launch FVP (fused.hip) applies
         for mode in (1, 0):
             set_option("chain", mode)
             e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
@@ -361,7 +362,8 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
             out[mode] = e.fvp(v, 0.0)
             e.close()
     finally:
-        set_option("chain", saved)
+        set_option("chain", saved[0])
+        set_option("fused", saved[1])
     assert_vec_close(out[1], ref, REL, f"chain Hv {obs} {hidden} {A}")
     assert_vec_close(out[1], out[0], REL, f"chain vs row-GEMM Hv {obs} {hidden} {A}")
 
