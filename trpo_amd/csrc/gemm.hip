@@ -710,39 +710,54 @@ rowgemm3_kernel(const RowGemmArgs args) {
   constexpr int AF4 = BM * BK / 4;          // f32x4 of A per k-tile
   constexpr int BC = NP * BN * (BK / 8);    // 16-B chunks of B planes per k-tile
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BC + NT - 1) / NT;
+  // Staging loads are buffer ops on per-segment descriptors (rows [m0, M) of A; the B planes): rows past
+  // M and k past the segment's K read 0 and invalid B columns address past the end, so a load is one
+  // instruction with a lane-constant voffset and a scalar k offset (no 64-bit address math, no selects).
+  constexpr int kOob = 0x40000000;
+  const int Mt = M - m0 < BM ? M - m0 : BM;
+  int vAo[AP], vBo[BP];
+  const int ldA = args.seg[0].lda;   // equal across segments (host check)
+#pragma unroll
+  for (int i = 0; i < AP; ++i) {
+    const int f = tid + i * NT;
+    const int r = f / (BK / 4), kq = f % (BK / 4);
+    vAo[i] = (AF4 % NT == 0 || f < AF4) ? (r * ldA + 4 * kq) * 4 : kOob;
+  }
+  const int ldkB = args.seg[0].ldk, planeB = args.seg[0].plane;   // equal across segments (host check)
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int f = tid + i * NT;
+    const int p = f / (BN * 2), rem = f % (BN * 2);
+    const int n = rem >> 1, kh = rem & 1;
+    const bool ok = (BC % NT == 0 || f < BC) && n0 + n < args.Npad;
+    vBo[i] = ok ? (p * planeB + (n0 + n) * ldkB + 8 * kh) * 2 : kOob;
+  }
   struct Stage {
     f32x4 ra[AP];
     u16x8 rb[BP];
-    bool oka[AP], okb[BP];
     bool s1;
   };
   auto gload = [&](Stage& st, int t) {
     const bool s1 = t >= nt0;
     st.s1 = s1;
     const GemmSeg& sg = s1 ? args.seg[1] : args.seg[0];
-    const float* Ap = sg.A;
-    const int lda = sg.lda, K = sg.K;
-    const uint16_t* B3 = sg.B3;
-    const int ldk = sg.ldk, plane = sg.plane;
+    const int K = sg.K;
     const int k0 = (s1 ? t - nt0 : t) * BK;
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(sg.A + (size_t)m0 * ldA), 0, Mt * ldA * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)sg.B3, 0, NP * planeB * 2, 0x00020000);
+    const bool kpart = k0 + BK > K;   // last k-tile of a segment whose K is not a multiple of BK
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
-      const int r = f / (BK / 4), kq = f % (BK / 4);
-      const int row = m0 + r, k = k0 + 4 * kq;
-      const bool ok = (AF4 % NT == 0 || f < AF4) && row < M && k < K;
-      st.ra[i] = *reinterpret_cast<const f32x4*>(Ap + (size_t)(ok ? row : 0) * lda + (ok ? k : 0));
-      st.oka[i] = ok;
+      const int kq = f % (BK / 4);
+      const int vo = (kpart && k0 + 4 * kq >= K) ? kOob : vAo[i];
+      st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, k0 * 4, 0));
     }
 #pragma unroll
-    for (int i = 0; i < BP; ++i) {
-      const int f = tid + i * NT;
-      const int p = f / (BN * 2), rem = f % (BN * 2);
-      const int n = rem >> 1, kh = rem & 1;
-      const bool ok = (BC % NT == 0 || f < BC) && n0 + n < args.Npad;
-      st.rb[i] = *reinterpret_cast<const u16x8*>(B3 + (ok ? (size_t)p * plane + (size_t)(n0 + n) * ldk + k0 + 8 * kh : 0));
-      st.okb[i] = ok;
-    }
+    for (int i = 0; i < BP; ++i)
+      st.rb[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rB, vBo[i], k0 * 2, 0));
   };
   auto sstore = [&](const Stage& st, int buf) {
     unsigned short* As = smem + buf * STG;
@@ -752,7 +767,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
       const int f = tid + i * NT;
       if (AF4 % NT == 0 || f < AF4) {
         const int r = f / (BK / 4), kq = f % (BK / 4);
-        const f32x4 x = st.oka[i] ? st.ra[i] : f32x4{};
+        const f32x4 x = st.ra[i];
         unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
         if constexpr (NP == 3) {
           u16x4 h, m, l;
@@ -788,7 +803,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
       if (BC % NT == 0 || f < BC) {
         const int p = f / (BN * 2), rem = f % (BN * 2);
         const int n = rem >> 1, kh = rem & 1;
-        *reinterpret_cast<u16x8*>(Bs + p * BPL + swz16(n, kh)) = st.okb[i] ? st.rb[i] : u16x8{};
+        *reinterpret_cast<u16x8*>(Bs + p * BPL + swz16(n, kh)) = st.rb[i];
       }
     }
   };
@@ -1751,6 +1766,10 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nseg; ++i)
     if (!a.seg[i].B3 || a.seg[i].ldk < ((a.seg[i].K + 15) / 16) * 16 || a.seg[i].ldk % 8)
       throw std::runtime_error("split-bf16 row GEMM: segment without B planes");
+  if (a.nseg > 1 && (a.seg[1].lda != a.seg[0].lda || a.seg[1].ldk != a.seg[0].ldk || a.seg[1].plane != a.seg[0].plane))
+    throw std::runtime_error("split-bf16 row GEMM: segments with different strides");
+  if ((int64_t)BM * a.seg[0].lda * 4 >= (int64_t(1) << 30) || (int64_t)(a.f16 ? 2 : 3) * a.seg[0].plane * 2 >= (int64_t(1) << 30))
+    throw std::runtime_error("split-bf16 row GEMM: operand beyond the buffer-descriptor range");
   const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
   if (a.f16)
     hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 2>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
