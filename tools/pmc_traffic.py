@@ -29,8 +29,8 @@ SPECS = {
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
-    "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 2, 2>",
-    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 2, 2>",
+    "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 1, 2>",
+    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 1, 2>",
 }
 
 
