@@ -27,6 +27,9 @@
 
 #ifndef TRPO_EPI_TRACK
 #define TRPO_EPI_TRACK 1   // ablation builds only (tools): 0 drops the f16 running-max tracking
+#ifndef TRPO_HEAD_LOG64
+#define TRPO_HEAD_LOG64 0  // 1: the loss heads' logs in f64 (round-1 form; A/B only)
+#endif
 #endif
 
 namespace trpo {
@@ -216,9 +219,16 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     double klp = 0.0, enp = 0.0;
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
+#if TRPO_HEAD_LOG64
       const double pd = p[t], od = old[t];
       klp += real[t] ? od * log((od + (double)kEps) / (pd + (double)kEps)) : 0.0;
       enp += real[t] ? -pd * log(pd + (double)kEps) : 0.0;
+#else
+      // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs, f64 row sums
+      const float lk = logf((old[t] + kEps) / (p[t] + kEps)), le = logf(p[t] + kEps);
+      klp += real[t] ? (double)old[t] * (double)lk : 0.0;
+      enp += real[t] ? -(double)p[t] * (double)le : 0.0;
+#endif
     }
     const double klt = hsum32d(klp);
     const double ent = hsum32d(enp);
