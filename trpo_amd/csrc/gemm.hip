@@ -25,6 +25,12 @@
 #include <stdexcept>
 #include <string>
 
+#ifndef TRPO_EPI_PIPE
+#define TRPO_EPI_PIPE 1    // 0: epilogue operand loads chunk by chunk (A/B builds only)
+#endif
+#ifndef TRPO_HEAD_DPP
+#define TRPO_HEAD_DPP 1    // 0: head row reductions by ds_bpermute shuffles (A/B builds only)
+#endif
 #ifndef TRPO_EPI_TRACK
 #define TRPO_EPI_TRACK 1   // ablation builds only (tools): 0 drops the f16 running-max tracking
 #ifndef TRPO_HEAD_LOG64
@@ -50,6 +56,54 @@ constexpr int BK = 16;
 
 __device__ __forceinline__ float one_minus_sq(float h) { return (1.0f - h) * (1.0f + h); }
 
+#if TRPO_HEAD_DPP
+// 32-lane (wave-half) reductions: the steps inside a 16-lane row are DPP moves (quad xor 1, quad
+// xor 2, half-row mirror, row mirror: after each step every lane of a 2^k group holds the group's
+// value, so the mirror partner sits in the other group), the cross-row step one ds_swizzle (xor 16).
+// Every lane ends with the same value (each step adds the same two operands on both partners).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned swz_x16(unsigned v) {
+  return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bitmask mode: and 0x1f, xor 0x10
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v))); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = dpp_u<CTRL>((unsigned)b), hi = dpp_u<CTRL>((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double swz_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = swz_x16((unsigned)b), hi = swz_x16((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+__device__ __forceinline__ float hsum32(float v) {
+  v += dpp_f<kDppX1>(v);
+  v += dpp_f<kDppX2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppMirror>(v);
+  return v + __uint_as_float(swz_x16(__float_as_uint(v)));
+}
+__device__ __forceinline__ double hsum32d(double v) {
+  v += dpp_d<kDppX1>(v);
+  v += dpp_d<kDppX2>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  v += dpp_d<kDppMirror>(v);
+  return v + swz_d(v);
+}
+__device__ __forceinline__ float hmax32(float v) {
+  v = fmaxf(v, dpp_f<kDppX1>(v));
+  v = fmaxf(v, dpp_f<kDppX2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppMirror>(v));
+  return fmaxf(v, __uint_as_float(swz_x16(__float_as_uint(v))));
+}
+#else
 __device__ __forceinline__ float hsum32(float v) {
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 32);
@@ -65,6 +119,7 @@ __device__ __forceinline__ float hmax32(float v) {
   for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 32));
   return v;
 }
+#endif
 
 // workgroup max of v[i] >= 0 for the non-NULL slots, one atomicMax per slot per workgroup (float bits
 // order as unsigned for v >= 0) into the slot's counter for this block (kernels.h, kAmaxSub).
@@ -375,36 +430,64 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
       auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
       };
+      // Operand loads run one (tm, tn) chunk ahead of the chunk being computed and stored: the
+      // chunk's loads are issued before the previous chunk's stores in program order (hipcc cannot
+      // prove the descriptors disjoint, so it would not hoist them itself), which leaves one chunk
+      // of loads in flight behind every chunk of math instead of a full round trip per chunk.
+      constexpr int NL = kRB ? 3 : (kUsesH ? 1 : 0);
+      constexpr int NCH = TM * TN;
+      float pre[2][NL > 0 ? NL : 1][16];
+      auto load_chunk = [&](int c, float (&dst)[NL > 0 ? NL : 1][16]) {
+        if constexpr (NL > 0) {
+          const int tn = c / TM, tm = c % TM;
+          const int vo = vbase + tn * 128;
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
+          for (int r = 0; r < 16; ++r) {
+            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+            dst[0][r] = ld(rH, vo, so);
+            if constexpr (NL == 3) {
+              dst[1][r] = ld(rE, vo, so);
+              dst[2][r] = ld(rRH, vo, so);
+            }
+          }
+        }
+      };
+      if constexpr (TRPO_EPI_PIPE) load_chunk(0, pre[0]);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int tn = c / TM, tm = c % TM;
         const int col = n0 + wn * TN * 32 + tn * 32 + lr;
         float bv = 0.0f;
         if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu)
           bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
         const int vo = vbase + tn * 128;
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
+        if constexpr (TRPO_EPI_PIPE) {
+          if (c + 1 < NCH) load_chunk(c + 1, pre[(c + 1) & 1]);
+        } else {
+          load_chunk(c, pre[c & 1]);
+        }
+        const float (&op)[NL > 0 ? NL : 1][16] = pre[c & 1];
+        {
           float o0[16], o1[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
             const float v = acc[tm][tn][r];
             if constexpr (EPI == (int)RowEpi::kTanh) {
               o0[r] = tanhf(v + bv);
             } else if constexpr (EPI == (int)RowEpi::kRHidden) {
-              o0[r] = one_minus_sq(ld(rH, vo, so)) * (v + bv);
+              o0[r] = one_minus_sq(op[0][r]) * (v + bv);
             } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
-              const float h = ld(rH, vo, so);
+              const float h = op[0][r];
               o0[r] = v * one_minus_sq(h);
               o1[r] = -2.0f * v * h;
             } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
-              o0[r] = v * one_minus_sq(ld(rH, vo, so));
+              o0[r] = v * one_minus_sq(op[0][r]);
             } else if constexpr (EPI == (int)RowEpi::kRelu) {
               o0[r] = fmaxf(v + bv, 0.0f);
             } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
-              o0[r] = ld(rH, vo, so) > 0.0f ? v : 0.0f;
+              o0[r] = op[0][r] > 0.0f ? v : 0.0f;
             } else {
-              o0[r] = fmaf(ld(rE, vo, so), ld(rRH, vo, so), v * one_minus_sq(ld(rH, vo, so)));
+              o0[r] = fmaf(op[1][r], op[2][r], v * one_minus_sq(op[0][r]));
             }
             // running max for the f16 operand scales (rows past M -- dropped stores -- hold 0 or,
             // for kRHidden, the tangent bias: harmless in a max)
