@@ -185,7 +185,11 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
  * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions), "fused"
  * (whole FVP incl. weight gradients in one launch of fused.hip for one or two hidden layers of
- * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups, the default).
+ * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups, the default),
+ * "low_seg" (f16 split GEMMs with two K-segments: a segment whose running-max product scale lies at
+ * least this many binades below the other's -- the O(eps) KL_ff plain-delta terms -- runs on one
+ * f16 product instead of three; 4 more binades when the dominant segment has an operand without a
+ * running max; 0 = off; default 14).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

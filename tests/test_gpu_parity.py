@@ -285,6 +285,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
     {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
+    {"low_seg": 0}, {"low_seg": 0, "chain": 0},               # every split segment on three products
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -292,7 +293,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain", "split_f16", "split_min_k", "fused")}
+                                           "split_wg", "chain", "split_f16", "split_min_k", "fused", "low_seg")}
     try:
         for k, v in opts.items():
             set_option(k, v)

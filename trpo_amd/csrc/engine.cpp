@@ -2193,6 +2193,7 @@ static int* option_slot(const std::string& k) {
   if (k == "graphs") return &g_options.graphs;
   if (k == "tail") return &g_options.tail;
   if (k == "fused") return &g_options.fused;
+  if (k == "low_seg") return &g_options.low_seg;
   throw ArgError("unknown option " + k);
 }
 

@@ -23,6 +23,7 @@
 #include "kernels.h"
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 
 #ifndef TRPO_EPI_PIPE
@@ -48,7 +49,7 @@ Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_in
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
                      env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
-                     env_int("TRPO_FUSED", 2)};
+                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14)};
 
 namespace {
 
@@ -793,6 +794,21 @@ rowgemm3_kernel(const RowGemmArgs args) {
     }
   }
   const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
+  // f16: a segment whose product scale is >= low_seg binades above the other's (its products are at
+  // most 2^(2 - low_seg) of the other segment's) runs on hi x hi alone: the dropped ah bl + al bh are
+  // 2^-10 of its own magnitude, 2^(-8 - low_seg) of the other segment's -- below the 3-product split's
+  // own 2^-22 at the default 14.  (The KL_ff plain-delta segments D_l V_l^T carry O(eps) terms.)
+  bool one0 = false, one1 = false;
+  if constexpr (NP == 2) {
+    if (args.low_seg > 0 && args.nseg > 1) {
+      // an operand without a running-max slot is scaled as if its max were 1 (tanh outputs): as the
+      // dominant segment's it may be far below that, so the gap must then be 4 binades wider
+      const int pen0 = (!args.seg[0].amaxA || !args.seg[0].amaxB) ? 4 : 0;
+      const int pen1 = (!args.seg[1].amaxA || !args.seg[1].amaxB) ? 4 : 0;
+      one0 = eP0 - eP1 >= args.low_seg + pen1;
+      one1 = eP1 - eP0 >= args.low_seg + pen0;
+    }
+  }
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -900,14 +916,23 @@ rowgemm3_kernel(const RowGemmArgs args) {
       }
     }
   };
-  auto compute = [&](int buf) {
+  auto compute_p = [&](int buf, auto one_c) {
+    constexpr bool ONE = decltype(one_c)::value;
     const unsigned short* As = smem + buf * STG;
     const unsigned short* Bs = As + NP * APL;
     // fragments streamed per output column tile to keep few registers live
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
-      if constexpr (NP == 3) {
+      if constexpr (NP == 2 && ONE) {
+        const f16x8 b0 = *reinterpret_cast<const f16x8*>(Bs + bo);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+          const f16x8 a0 = *reinterpret_cast<const f16x8*>(As + ao);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[tm][tn], 0, 0, 0);
+        }
+      } else if constexpr (NP == 3) {
         bf16x8 b[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
@@ -946,6 +971,10 @@ rowgemm3_kernel(const RowGemmArgs args) {
       }
     }
   };
+  auto compute = [&](int buf, int t) {
+    if (t >= nt0 ? one1 : one0) compute_p(buf, std::true_type{});
+    else compute_p(buf, std::false_type{});
+  };
   // f16: when the k-tiles move from segment 0 to segment 1, bring the accumulator to segment 1's
   // product scale (powers of two: exact)
   auto seg_switch = [&](int t) {
@@ -968,7 +997,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
         seg_switch(t);
-        compute(t & 1);
+        compute(t & 1, t);
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
         lds_barrier();
       }
@@ -983,18 +1012,18 @@ rowgemm3_kernel(const RowGemmArgs args) {
       for (; t + 1 < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
         seg_switch(t);
-        compute(0);
+        compute(0, t);
         sstore(S1, 1);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
         seg_switch(t + 1);
-        compute(1);
+        compute(1, t + 1);
         if (t + 2 < ntiles) sstore(S0, 0);
         lds_barrier();
       }
       if (t < ntiles) {
         seg_switch(t);
-        compute(0);
+        compute(0, t);
       }
     }
   }
@@ -1036,6 +1065,17 @@ wgrad3_kernel(const WGradArgs args) {
     for (int g = 0; g < args.nseg && g < 2; ++g) {
       eA[g] = amax_exp(args.seg[g].amaxA);
       eB[g] = amax_exp(args.seg[g].amaxB);
+    }
+  }
+  // f16: one product for a segment >= low_seg binades below the other (see rowgemm3_kernel)
+  bool one0 = false, one1 = false;
+  if constexpr (NP == 2) {
+    if (args.low_seg > 0 && args.nseg > 1) {
+      const int d = (eA[1] + eB[1]) - (eA[0] + eB[0]);
+      const int pen0 = (!args.seg[0].amaxA || !args.seg[0].amaxB) ? 4 : 0;   // as in rowgemm3_kernel
+      const int pen1 = (!args.seg[1].amaxA || !args.seg[1].amaxB) ? 4 : 0;
+      one0 = -d >= args.low_seg + pen1;
+      one1 = d >= args.low_seg + pen0;
     }
   }
 
@@ -1153,13 +1193,22 @@ wgrad3_kernel(const WGradArgs args) {
       }
     }
   };
-  auto compute = [&](int buf) {
+  auto compute_p = [&](int buf, auto one_c) {
+    constexpr bool ONE = decltype(one_c)::value;
     const unsigned short* As = smem + buf * STG;
     const unsigned short* Bs = As + NP * APL;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
-      if constexpr (NP == 3) {
+      if constexpr (NP == 2 && ONE) {
+        const f16x8 b0 = *reinterpret_cast<const f16x8*>(Bs + bo);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+          const f16x8 a0 = *reinterpret_cast<const f16x8*>(As + ao);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[tm][tn], 0, 0, 0);
+        }
+      } else if constexpr (NP == 3) {
         bf16x8 b[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Bs + p * BPL + bo);
@@ -1197,6 +1246,10 @@ wgrad3_kernel(const WGradArgs args) {
       }
     }
   };
+  auto compute = [&](int buf, int t) {
+    if (t >= nk ? one1 : one0) compute_p(buf, std::true_type{});
+    else compute_p(buf, std::false_type{});
+  };
   auto seg_switch = [&](int t) {
     if constexpr (NP == 2) {
       if (t == nk && args.nseg > 1) {
@@ -1215,7 +1268,7 @@ wgrad3_kernel(const WGradArgs args) {
       for (int t = 0; t < ntiles; ++t) {
         if (t + 1 < ntiles) gload(S, t + 1);
         seg_switch(t);
-        compute(t & 1);
+        compute(t & 1, t);
         if (t + 1 < ntiles) sstore(S, (t + 1) & 1);
         lds_barrier();
       }
@@ -1229,18 +1282,18 @@ wgrad3_kernel(const WGradArgs args) {
       for (; t + 1 < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);
         seg_switch(t);
-        compute(0);
+        compute(0, t);
         sstore(S1, 1);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
         seg_switch(t + 1);
-        compute(1);
+        compute(1, t + 1);
         if (t + 2 < ntiles) sstore(S0, 0);
         lds_barrier();
       }
       if (t < ntiles) {
         seg_switch(t);
-        compute(0);
+        compute(0, t);
       }
     }
   }
@@ -1864,9 +1917,11 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
   if ((int64_t)BM * a.seg[0].lda * 4 >= (int64_t(1) << 30) || (int64_t)(a.f16 ? 2 : 3) * a.seg[0].plane * 2 >= (int64_t(1) << 30))
     throw std::runtime_error("split-bf16 row GEMM: operand beyond the buffer-descriptor range");
   const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
+  RowGemmArgs b = a;
+  b.low_seg = g_options.low_seg;
   if (a.f16)
     hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 2>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
-                       s, a);
+                       s, b);
   else
     hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 3>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
                        s, a);
@@ -1957,8 +2012,10 @@ void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
   if ((int64_t)a.rows_per_split * (a.seg[0].lda > a.seg[0].ldb ? a.seg[0].lda : a.seg[0].ldb) * 4 >= (int64_t(1) << 30))
     throw std::runtime_error("split-bf16 wgrad: a split's rows exceed the 1 GiB buffer-descriptor range");
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
+  WGradArgs b = a;
+  b.low_seg = g_options.low_seg;
   if (a.f16)
-    hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 2>), grid, dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 2>), grid, dim3(WM * WN * 64), 0, s, b);
   else
     hipLaunchKernelGGL((wgrad3_kernel<WM, WN, TM, TN, OCC, PF, 3>), grid, dim3(WM * WN * 64), 0, s, a);
 }

@@ -26,6 +26,8 @@ struct Options {
   int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
   int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
   int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves (default)
+  int low_seg;     // f16 split GEMMs: a segment whose product scale sits >= low_seg binades below the other
+                   // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -108,6 +110,7 @@ struct RowGemmArgs {
   RowEpi epi;
   RowEpiArgs ea;
   int f16 = 0;         // split path: 1 = two scaled f16 planes / 3 products, 0 = three bf16 planes / 6
+  int low_seg = 0;     // f16: binade gap that puts the smaller segment on one product (0 = off; set at launch)
 };
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
@@ -156,6 +159,7 @@ struct WGradArgs {
   int64_t off_w, off_b;
   const int* skip;
   int f16 = 0;         // split path: scaled f16 (3 products) instead of bf16 (6 products)
+  int low_seg = 0;     // f16: as RowGemmArgs::low_seg (set at launch)
 };
 
 void launch_wgrad(const WGradArgs& a, hipStream_t s);
