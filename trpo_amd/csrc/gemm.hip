@@ -29,6 +29,9 @@
 #ifndef TRPO_EPI_PIPE
 #define TRPO_EPI_PIPE 1    // 0: epilogue operand loads chunk by chunk (A/B builds only)
 #endif
+#ifndef TRPO_FAST_TANH
+#define TRPO_FAST_TANH 1   // 0: the device library's tanhf in the forward epilogues (A/B builds only)
+#endif
 #ifndef TRPO_HEAD_DPP
 #define TRPO_HEAD_DPP 1    // 0: head row reductions by ds_bpermute shuffles (A/B builds only)
 #endif
@@ -56,6 +59,30 @@ namespace {
 constexpr int BK = 16;
 
 __device__ __forceinline__ float one_minus_sq(float h) { return (1.0f - h) * (1.0f + h); }
+
+// tanh for the forward epilogues (trpo_inksci.py:38 `tanh` layers), branch-free: both forms are
+// evaluated and one selected, where the device library's tanhf branches per lane (a wave runs both
+// sides under exec masks, ~35 VALU per element, which made the tanh epilogue ~2 ms of a 256-wide
+// C4 forward GEMM).  |x| < 0.625: x + x^3 P(x^2), the minimax odd polynomial of the device library's
+// own small-argument branch; otherwise (1 - t) / (1 + t) with t = 2^(-2|x| log2 e) from v_exp_f32
+// and v_rcp_f32 (a few ulp; t underflows to 0 past |x| ~ 44, giving 1).  Sign restored last.
+__device__ __forceinline__ float tanh_fast(float x) {
+#if TRPO_FAST_TANH
+  const float ax = fabsf(x);
+  const float x2 = x * x;
+  float p = __builtin_fmaf(-0.005700020585209131f, x2, 0.02063407190144062f);   // 0xbbbac73d, 0x3ca908c9
+  p = __builtin_fmaf(p, x2, -0.053737930953502655f);                        // 0xbd5c1c4e
+  p = __builtin_fmaf(p, x2, 0.13331416249275208f);                         // 0x3e088382
+  p = __builtin_fmaf(p, x2, -0.3333328068256378f);                        // 0xbeaaaa99
+  const float small = __builtin_fmaf(x2, ax * p, ax);
+  const float t = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);   // 2^(-2|x| log2 e) = e^(-2|x|)
+  const float r = __builtin_amdgcn_rcpf(1.0f + t);
+  const float big = __builtin_fmaf(-t, r, r);                          // (1 - t) / (1 + t)
+  return __builtin_copysignf(ax < 0.625f ? small : big, x);
+#else
+  return tanhf(x);
+#endif
+}
 
 #if TRPO_HEAD_DPP
 // 32-lane (wave-half) reductions: the steps inside a 16-lane row are DPP moves (quad xor 1, quad
@@ -159,7 +186,7 @@ template <int EPI>
 __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, bool real, float v) {
   const size_t idx = (size_t)row * e.ldo + col;
   if constexpr (EPI == (int)RowEpi::kTanh) {
-    e.out0[idx] = real ? tanhf(v + e.bias[col]) : 0.0f;
+    e.out0[idx] = real ? tanh_fast(v + e.bias[col]) : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kRHidden) {
     e.out0[idx] = real ? one_minus_sq(e.H[idx]) * (v + e.bias[col]) : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
@@ -191,7 +218,7 @@ template <int EPI>
 __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool /*real*/, float v, float bv,
                                            float& o0, float& o1) {
   if constexpr (EPI == (int)RowEpi::kTanh) {
-    o0 = tanhf(v + bv);
+    o0 = tanh_fast(v + bv);
   } else if constexpr (EPI == (int)RowEpi::kRHidden) {
     o0 = one_minus_sq(e.H[idx]) * (v + bv);
   } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
@@ -474,7 +501,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
           for (int r = 0; r < 16; ++r) {
             const float v = acc[tm][tn][r];
             if constexpr (EPI == (int)RowEpi::kTanh) {
-              o0[r] = tanhf(v + bv);
+              o0[r] = tanh_fast(v + bv);
             } else if constexpr (EPI == (int)RowEpi::kRHidden) {
               o0[r] = one_minus_sq(op[0][r]) * (v + bv);
             } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
