@@ -764,11 +764,13 @@ struct trpo_engine {
       seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
       a.seg[0].amaxA = am_d(l);
       a.seg[0].amaxB = am_w(l);
-      a.epi = RowEpi::kPrepBwd;
+      // D_0 (the plain delta below the first hidden layer) has no reader: the R-backward stops at
+      // RD_0 and the layer-0 weight R-gradient is X^T RD_0, so only E_0 is written there
+      a.epi = l > 1 ? RowEpi::kPrepBwd : RowEpi::kPrepBwdE;
       a.ea.H = H[l];
-      a.ea.out0 = D[l - 1];
-      a.ea.amax0 = am_d(l - 1);
-      a.ea.out1 = E[l - 1];
+      a.ea.out0 = l > 1 ? D[l - 1] : E[0];
+      a.ea.amax0 = l > 1 ? am_d(l - 1) : nullptr;
+      a.ea.out1 = l > 1 ? E[l - 1] : nullptr;
       a.ea.ldo = wp[l];
       char t[32];
       std::snprintf(t, sizeof t, "bwd_l%d", l);

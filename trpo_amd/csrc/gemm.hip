@@ -198,6 +198,8 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
       e.out0[idx] = 0.0f;
       e.out1[idx] = 0.0f;
     }
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
+    e.out0[idx] = real ? -2.0f * v * e.H[idx] : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
     e.out0[idx] = real ? v * one_minus_sq(e.H[idx]) : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
@@ -225,6 +227,8 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
     const float h = e.H[idx];
     o0 = v * one_minus_sq(h);
     o1 = -2.0f * v * h;
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
+    o0 = -2.0f * v * e.H[idx];
   } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
     o0 = v * one_minus_sq(e.H[idx]);
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
@@ -441,6 +445,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
         return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
       };
       constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
+                              EPI == (int)RowEpi::kPrepBwdE ||
                               EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd ||
                               EPI == (int)RowEpi::kReluBwd;
       constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
@@ -508,6 +513,8 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
               const float h = op[0][r];
               o0[r] = v * one_minus_sq(h);
               o1[r] = -2.0f * v * h;
+            } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
+              o0[r] = -2.0f * v * op[0][r];
             } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
               o0[r] = v * one_minus_sq(op[0][r]);
             } else if constexpr (EPI == (int)RowEpi::kRelu) {
@@ -520,7 +527,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
             // running max for the f16 operand scales (rows past M -- dropped stores -- hold 0 or,
             // for kRHidden, the tangent bias: harmless in a max)
             if constexpr (TRPO_EPI_TRACK && EPI != (int)RowEpi::kTanh && EPI != (int)RowEpi::kRelu &&
-                          EPI != (int)RowEpi::kReluBwd) {
+                          EPI != (int)RowEpi::kReluBwd && EPI != (int)RowEpi::kPrepBwdE) {
               mx0 = fmaxf(mx0, fabsf(o0[r]));
               if constexpr (EPI == (int)RowEpi::kPrepBwd) mx1 = fmaxf(mx1, fabsf(o1[r]));
             }
@@ -2072,6 +2079,7 @@ void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
     case RowEpi::kRHidden: launch_row_epi<(int)RowEpi::kRHidden>(a, s); break;
     case RowEpi::kPrepBwd: launch_row_epi<(int)RowEpi::kPrepBwd>(a, s); break;
     case RowEpi::kPgBwd: launch_row_epi<(int)RowEpi::kPgBwd>(a, s); break;
+    case RowEpi::kPrepBwdE: launch_row_epi<(int)RowEpi::kPrepBwdE>(a, s); break;
     case RowEpi::kRBwd: launch_row_epi<(int)RowEpi::kRBwd>(a, s); break;
     case RowEpi::kPrepHead: launch_row_epi<(int)RowEpi::kPrepHead>(a, s); break;
     case RowEpi::kLossHead: launch_row_epi<(int)RowEpi::kLossHead>(a, s); break;

@@ -74,6 +74,8 @@ enum class RowEpi : int {
   kRHead = 7,     // R-softmax head: RD_L                        (FVP)
   kRelu = 8,      // out = max(acc + bias, 0)                    (VF forward, utils.py:60-61)
   kReluBwd = 9,   // out = acc * (H > 0), H = the ReLU output    (VF backward)
+  kPrepBwdE = 10, // E = -2 acc H only                           (KL_ff plain backward into the first
+                  //                                              hidden layer: D_0 has no reader)
 };
 // the row-wise softmax heads (one output row per 32-lane wave half, up to kMaxHeadTiles 32-column tiles)
 constexpr int kMaxHeadTiles = 4;
