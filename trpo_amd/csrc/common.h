@@ -47,6 +47,61 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n, do
 }
 
 
+// ---- lane reductions on DPP moves (no LDS round trips) --------------------------------------
+// Inside a 16-lane row: quad xor 1, quad xor 2, half-row mirror, row mirror.  After each step every
+// lane of a 2^k group holds the group's value, so the mirror partner sits in the other group; every
+// lane ends with the same value (both partners add the same two operands).  Across the two rows of a
+// 32-lane half: one ds_swizzle (bitmask mode, xor 16).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned swz_x16(unsigned v) {
+  return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // and 0x1f, xor 0x10
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v))); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = dpp_u<CTRL>((unsigned)b), hi = dpp_u<CTRL>((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float swz_f(float v) { return __uint_as_float(swz_x16(__float_as_uint(v))); }
+__device__ __forceinline__ double swz_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = swz_x16((unsigned)b), hi = swz_x16((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+__device__ __forceinline__ float sum16_dpp(float v) {
+  v += dpp_f<kDppX1>(v);
+  v += dpp_f<kDppX2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  return v + dpp_f<kDppMirror>(v);
+}
+__device__ __forceinline__ double sum16_dpp(double v) {
+  v += dpp_d<kDppX1>(v);
+  v += dpp_d<kDppX2>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  return v + dpp_d<kDppMirror>(v);
+}
+__device__ __forceinline__ float sum32_dpp(float v) {
+  v = sum16_dpp(v);
+  return v + swz_f(v);
+}
+__device__ __forceinline__ double sum32_dpp(double v) {
+  v = sum16_dpp(v);
+  return v + swz_d(v);
+}
+__device__ __forceinline__ float max32_dpp(float v) {
+  v = fmaxf(v, dpp_f<kDppX1>(v));
+  v = fmaxf(v, dpp_f<kDppX2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppMirror>(v));
+  return fmaxf(v, swz_f(v));
+}
+
 // Workgroup barrier for an LDS hand-off only: waits for this wave's LDS operations,
 // not for its outstanding global loads.  __syncthreads() also emits vmcnt(0), which
 // would drain a register prefetch that is meant to stay in flight across the barrier.

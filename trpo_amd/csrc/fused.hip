@@ -219,12 +219,7 @@ __global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs f
           f32x4 v = R[t];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float x = v[j];
-            x += __shfl_xor(x, 1, 16);
-            x += __shfl_xor(x, 2, 16);
-            x += __shfl_xor(x, 4, 16);
-            x += __shfl_xor(x, 8, 16);
-            v[j] = x;
+            v[j] = sum16_dpp(v[j]);   // the wave's 16 states of lane group g (common.h: DPP moves)
           }
           if (s == 0) {
 #pragma unroll

@@ -85,52 +85,10 @@ __device__ __forceinline__ float tanh_fast(float x) {
 }
 
 #if TRPO_HEAD_DPP
-// 32-lane (wave-half) reductions: the steps inside a 16-lane row are DPP moves (quad xor 1, quad
-// xor 2, half-row mirror, row mirror: after each step every lane of a 2^k group holds the group's
-// value, so the mirror partner sits in the other group), the cross-row step one ds_swizzle (xor 16).
-// Every lane ends with the same value (each step adds the same two operands on both partners).
-template <int CTRL>
-__device__ __forceinline__ unsigned dpp_u(unsigned v) {
-  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ unsigned swz_x16(unsigned v) {
-  return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bitmask mode: and 0x1f, xor 0x10
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) { return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v))); }
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = dpp_u<CTRL>((unsigned)b), hi = dpp_u<CTRL>((unsigned)(b >> 32));
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double swz_d(double v) {
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = swz_x16((unsigned)b), hi = swz_x16((unsigned)(b >> 32));
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
-__device__ __forceinline__ float hsum32(float v) {
-  v += dpp_f<kDppX1>(v);
-  v += dpp_f<kDppX2>(v);
-  v += dpp_f<kDppHalfMirror>(v);
-  v += dpp_f<kDppMirror>(v);
-  return v + __uint_as_float(swz_x16(__float_as_uint(v)));
-}
-__device__ __forceinline__ double hsum32d(double v) {
-  v += dpp_d<kDppX1>(v);
-  v += dpp_d<kDppX2>(v);
-  v += dpp_d<kDppHalfMirror>(v);
-  v += dpp_d<kDppMirror>(v);
-  return v + swz_d(v);
-}
-__device__ __forceinline__ float hmax32(float v) {
-  v = fmaxf(v, dpp_f<kDppX1>(v));
-  v = fmaxf(v, dpp_f<kDppX2>(v));
-  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
-  v = fmaxf(v, dpp_f<kDppMirror>(v));
-  return fmaxf(v, __uint_as_float(swz_x16(__float_as_uint(v))));
-}
+// 32-lane (wave-half) reductions on DPP moves + one ds_swizzle (common.h)
+__device__ __forceinline__ float hsum32(float v) { return sum32_dpp(v); }
+__device__ __forceinline__ double hsum32d(double v) { return sum32_dpp(v); }
+__device__ __forceinline__ float hmax32(float v) { return max32_dpp(v); }
 #else
 __device__ __forceinline__ float hsum32(float v) {
 #pragma unroll

@@ -43,11 +43,18 @@ constexpr int SLD = 36;      // row stride (floats) of the [row][action] LDS til
 
 __device__ __forceinline__ float omsq(float h) { return (1.0f - h) * (1.0f + h); }
 
+#ifndef TRPO_TAIL_DPP
+#define TRPO_TAIL_DPP 1    // 0: R-softmax row sums by ds_bpermute shuffles (A/B builds only)
+#endif
 template <class T>
 __device__ __forceinline__ T hsum32t(T v) {
+#if TRPO_TAIL_DPP
+  return sum32_dpp(v);   // common.h: DPP moves + one ds_swizzle
+#else
 #pragma unroll
   for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 32);
   return v;
+#endif
 }
 #ifndef TRPO_TAIL_HEAD64
 #define TRPO_TAIL_HEAD64 0
