@@ -34,10 +34,8 @@ __host__ __device__ constexpr int chain_perm(int kk) {
 
 __device__ __forceinline__ float c_one_minus_sq(float h) { return (1.0f - h) * (1.0f + h); }
 
-__device__ __forceinline__ double sum4lanes(double v) {   // lanes s, s+16, s+32, s+48
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+__device__ __forceinline__ double sum4lanes(double v) {   // lanes s, s+16, s+32, s+48 (common.h swaps)
+  return xadd_d<true>(xadd_d<false>(v));
 }
 
 // B operand (3 bf16 planes) of v_mfma_f32_16x16x32_bf16 from two acc-layout tiles: lane (g, s)

@@ -51,13 +51,10 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n, do
 // Inside a 16-lane row: quad xor 1, quad xor 2, half-row mirror, row mirror.  After each step every
 // lane of a 2^k group holds the group's value, so the mirror partner sits in the other group; every
 // lane ends with the same value (both partners add the same two operands).  Across the two rows of a
-// 32-lane half: one ds_swizzle (bitmask mode, xor 16).
+// 32-lane half: v_permlane16_swap (below).
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u(unsigned v) {
   return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ unsigned swz_x16(unsigned v) {
-  return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // and 0x1f, xor 0x10
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) { return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v))); }
@@ -67,11 +64,40 @@ __device__ __forceinline__ double dpp_d(double v) {
   const unsigned lo = dpp_u<CTRL>((unsigned)b), hi = dpp_u<CTRL>((unsigned)(b >> 32));
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ float swz_f(float v) { return __uint_as_float(swz_x16(__float_as_uint(v))); }
-__device__ __forceinline__ double swz_d(double v) {
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = swz_x16((unsigned)b), hi = swz_x16((unsigned)(b >> 32));
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+// v_permlane16_swap / v_permlane32_swap with both operands = v: the pair holds, in some order, this
+// lane's value and that of lane l ^ 16 (resp. l ^ 32), so their sum / max is the same on both partners.
+template <bool X32>
+__device__ __forceinline__ void pair_u(unsigned v, unsigned& a, unsigned& b) {
+  if constexpr (X32) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    a = p[0];
+    b = p[1];
+  } else {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    a = p[0];
+    b = p[1];
+  }
+}
+template <bool X32>
+__device__ __forceinline__ float xadd_f(float v) {
+  unsigned a, b;
+  pair_u<X32>(__float_as_uint(v), a, b);
+  return __uint_as_float(a) + __uint_as_float(b);
+}
+template <bool X32>
+__device__ __forceinline__ float xmax_f(float v) {
+  unsigned a, b;
+  pair_u<X32>(__float_as_uint(v), a, b);
+  return fmaxf(__uint_as_float(a), __uint_as_float(b));
+}
+template <bool X32>
+__device__ __forceinline__ double xadd_d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  unsigned la, lb, ha, hb;
+  pair_u<X32>((unsigned)u, la, lb);
+  pair_u<X32>((unsigned)(u >> 32), ha, hb);
+  return __builtin_bit_cast(double, ((unsigned long long)ha << 32) | la) +
+         __builtin_bit_cast(double, ((unsigned long long)hb << 32) | lb);
 }
 constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
 __device__ __forceinline__ float sum16_dpp(float v) {
@@ -86,20 +112,14 @@ __device__ __forceinline__ double sum16_dpp(double v) {
   v += dpp_d<kDppHalfMirror>(v);
   return v + dpp_d<kDppMirror>(v);
 }
-__device__ __forceinline__ float sum32_dpp(float v) {
-  v = sum16_dpp(v);
-  return v + swz_f(v);
-}
-__device__ __forceinline__ double sum32_dpp(double v) {
-  v = sum16_dpp(v);
-  return v + swz_d(v);
-}
+__device__ __forceinline__ float sum32_dpp(float v) { return xadd_f<false>(sum16_dpp(v)); }
+__device__ __forceinline__ double sum32_dpp(double v) { return xadd_d<false>(sum16_dpp(v)); }
 __device__ __forceinline__ float max32_dpp(float v) {
   v = fmaxf(v, dpp_f<kDppX1>(v));
   v = fmaxf(v, dpp_f<kDppX2>(v));
   v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
   v = fmaxf(v, dpp_f<kDppMirror>(v));
-  return fmaxf(v, swz_f(v));
+  return xmax_f<false>(v);
 }
 
 // Workgroup barrier for an LDS hand-off only: waits for this wave's LDS operations,
