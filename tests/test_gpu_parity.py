@@ -611,3 +611,47 @@ def test_many_actions_vs_oracle(gpu_available, obs, hidden, A, n):
     assert st["k"] == r.k
     assert_vec_close(e.get_flat(), r.theta_new, REL, f"theta A={A}")
     e.close()
+
+
+@pytest.mark.parametrize("scale", [6.0, 25.0], ids=["peaked", "saturated"])
+@pytest.mark.parametrize("low_seg", [14, 0], ids=["low_seg", "three_products"])
+def test_saturated_softmax_fvp_vs_oracle(gpu_available, scale, low_seg):
+    """C4 layer shapes with the head's weights scaled up until the softmax is near-deterministic: many
+    p_j fall to or below eps, the O(eps) KL_ff terms (D_l, E_l) become comparable to the R-terms, and
+    the one-product low segment (option low_seg) must fall back to three products by its own binade
+    test.  Undamped FVP and one update against the float64 oracle (trpo_inksci.py:56-70)."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import VEC_STEPDIR, get_option, set_option
+    spec = O.PolicySpec(128, [256, 256], 18)
+    n = 3000
+    d = O.synthetic_batch(spec, n, seed=21)
+    params = O.unflatten(d["theta"].astype(np.float64).copy(), spec)
+    W, b = params[-1]
+    W *= scale
+    b *= scale
+    theta = O.flatten(params).astype(np.float32)
+    old = O.action_dist(theta.astype(np.float64), d["X"], spec, np.float64).astype(np.float32)
+    assert (old < 1e-6).mean() > (0.2 if scale > 10 else 0.01)   # the regime this test is about
+    # actions drawn from the policy, as a rollout would (a uniform draw would hit p_old[a] = 0 in f32,
+    # where the reference's un-eps'd ratio p/p_old is inf and every result NaN: test_gpu_degenerate.py)
+    u = np.random.RandomState(23).uniform(size=(n, 1))
+    d["actions"] = np.minimum((np.cumsum(old.astype(np.float64), axis=1) < u).sum(axis=1), spec.n_actions - 1)
+    assert old[np.arange(n), d["actions"]].min() > 0
+    saved = get_option("low_seg")
+    set_option("low_seg", low_seg)
+    try:
+        eng = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+        eng.set_flat(theta)
+        eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), old)
+        v = np.random.RandomState(22).standard_normal(spec.n_params).astype(np.float32)
+        hv = eng.fvp(v, 0.0)
+        ref = O.fvp_undamped(theta.astype(np.float64), d["X"], v.astype(np.float64), spec)
+        assert_vec_close(hv, ref, REL, "Hv")
+        st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+        r = O.trpo_update(theta.astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], old),
+                          spec, np.float64, 10, 0.0)
+        assert st["k"] == r.k
+        assert_vec_close(eng.get_vector(VEC_STEPDIR), r.stepdir, REL, "stepdir")
+        eng.close()
+    finally:
+        set_option("low_seg", saved)
