@@ -110,6 +110,10 @@ struct trpo_engine {
     return g_options.tail != 0 && f16 && split_on() && L >= 2 && !fused_head && !head_bwd &&
            tail_eligible(wp[L - 1], wp[L]) && w[L] <= 32;
   }
+  // whether the FVP path reads E_{L-2} (the plain tanh'' term under the last hidden layer): every path
+  // but the fused tail, which recomputes it (tail.hip)
+  bool e_top_needed() const { return L < 2 || !use_tail() || use_fused() || use_chain(); }
+  bool prep_e_top = true;    // prepare() wrote E_{L-2}
   bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
   bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
@@ -756,21 +760,26 @@ struct trpo_engine {
     am_reset(am_d(0), L);
     am_reset(am_ds(L - 1), 1);
     forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
-    // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H
+    // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H.
+    // Only what the FVP path will read is written (prep_e_top records it; fvp() re-prepares if the
+    // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
+    // recomputes it from H and D_{L-1}.
+    prep_e_top = e_top_needed();
     for (int l = L - 1; l >= 1; --l) {
+      const bool need_d = l > 1, need_e = l < L - 1 || prep_e_top;
+      if (!need_d && !need_e) continue;
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{D[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
       seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
       a.seg[0].amaxA = am_d(l);
       a.seg[0].amaxB = am_w(l);
-      // D_0 (the plain delta below the first hidden layer) has no reader: the R-backward stops at
-      // RD_0 and the layer-0 weight R-gradient is X^T RD_0, so only E_0 is written there
-      a.epi = l > 1 ? RowEpi::kPrepBwd : RowEpi::kPrepBwdE;
+      // both: kPrepBwd ; E only (D_0): kPrepBwdE ; D only: kPgBwd, whose epilogue is DH (1-H^2)
+      a.epi = need_d ? (need_e ? RowEpi::kPrepBwd : RowEpi::kPgBwd) : RowEpi::kPrepBwdE;
       a.ea.H = H[l];
-      a.ea.out0 = l > 1 ? D[l - 1] : E[0];
-      a.ea.amax0 = l > 1 ? am_d(l - 1) : nullptr;
-      a.ea.out1 = l > 1 ? E[l - 1] : nullptr;
+      a.ea.out0 = need_d ? D[l - 1] : E[l - 1];
+      a.ea.amax0 = need_d ? am_d(l - 1) : nullptr;
+      a.ea.out1 = need_d && need_e ? E[l - 1] : nullptr;
       a.ea.ldo = wp[l];
       char t[32];
       std::snprintf(t, sizeof t, "bwd_l%d", l);
@@ -854,6 +863,7 @@ struct trpo_engine {
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
   void fvp(const float* v, float* out, const int* skip) {
+    if (prepared && e_top_needed() && !prep_e_top) prepared = false;   // the path changed since prepare()
     prepare();
     if (use_fused()) {
       fvp_fused(v, out, skip);
@@ -1322,7 +1332,7 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, have_returns;
+    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top;
   } upd_flags{};
   void drop_graph() {
     if (upd_exec) {
@@ -1349,6 +1359,7 @@ struct trpo_engine {
       w3_valid = upd_flags.w3_valid;
       chain_w_valid = upd_flags.chain_w_valid;
       have_returns = upd_flags.have_returns;
+      prep_e_top = upd_flags.prep_e_top;
       return;
     }
     if (!same) {
@@ -1383,7 +1394,7 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns};
+    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;
