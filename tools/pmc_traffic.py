@@ -48,8 +48,10 @@ def load(path, counter):
 def pick(rows, sub, period=None, phase=None, longest=False):
     sel = [r for r in rows if sub in r[1]]
     if longest and sel:
-        dmax = max(r[3] for r in sel)
-        sel = [r for r in sel if r[3] > 0.75 * dmax]
+        # the FVP launches are the majority: keep those near the median duration (a single dispatch
+        # slowed down under the counters must not become the reference)
+        dmed = statistics.median(r[3] for r in sel)
+        sel = [r for r in sel if r[3] > 0.75 * dmed]
     elif period:
         sel = [r for i, r in enumerate(sel) if i % period == phase]
     return sel
