@@ -749,9 +749,14 @@ __device__ __forceinline__ void scale_acc(f32x16 (&acc)[TM][TN], int e) {
 }
 
 // LDS images are [row][16 k] bf16 (32-B rows, no padding); the two 16-B k-chunks of
-// a row swap places on odd 8-row groups, so the 16 lanes of a ds_read_b128 phase
-// (rows r..r+15, one chunk) hit 16 distinct bank groups.
-__device__ __forceinline__ int swz16(int row, int chunk) { return row * 16 + ((chunk ^ ((row >> 3) & 1)) << 3); }
+// a row swap places where bit 2 ^ bit 3 of the row is set.
+// (The flip bit is bit 2 ^ bit 3 of the row: the ds_read_b128 fragment reads, serviced in the lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), put their 16 rows on 16 distinct 16-B bank slots, and so do the
+// weight-gradient staging stores -- ds_write_b128, 8 lanes per LDS cycle on 32 banks, 8 consecutive rows of one
+// chunk -- which a bit-3-only flip left 2-way conflicted, rows r and r+4 on the same banks.)
+__device__ __forceinline__ int swz16(int row, int chunk) {
+  return row * 16 + ((chunk ^ (((row >> 2) ^ (row >> 3)) & 1)) << 3);
+}
 
 template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF, int NP>
 __global__ void __launch_bounds__(WM* WN * 64, OCC)   // OCC waves / SIMD
