@@ -655,3 +655,30 @@ def test_saturated_softmax_fvp_vs_oracle(gpu_available, scale, low_seg):
         eng.close()
     finally:
         set_option("low_seg", saved)
+
+
+def test_path_switch_after_prepare_rewrites_e(gpu_available):
+    """Under the fused tail the prepare pass skips E_{L-2} (tail.hip recomputes it); switching the same
+    engine to the per-layer R-backward afterwards must re-prepare rather than read an E that was never
+    written (engine.cpp fvp(), prep_e_top)."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(128, [256, 256], 18)
+    n = 2000
+    d = O.synthetic_batch(spec, n, seed=31)
+    v = np.random.RandomState(32).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(d["theta"].astype(np.float64), d["X"], v.astype(np.float64), spec)
+    saved = get_option("tail")
+    try:
+        set_option("tail", 1)
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+        e.set_flat(d["theta"])
+        e.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+        assert_vec_close(e.fvp(v, 0.0), ref, REL, "Hv, fused tail")
+        set_option("tail", 0)
+        assert_vec_close(e.fvp(v, 0.0), ref, REL, "Hv, per-layer after the switch")
+        set_option("tail", 1)
+        assert_vec_close(e.fvp(v, 0.0), ref, REL, "Hv, back on the tail")
+        e.close()
+    finally:
+        set_option("tail", saved)
