@@ -42,6 +42,7 @@ reports nproc, the affinity mask and any cgroup quota) and extrapolates linearly
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -192,7 +193,6 @@ def tag_roof(tag: str, widths, n: int):
 
 def committed_traffic(config: str, rows: int, tag: str):
     """Per-launch HBM bytes of `tag` from the newest matching profiles/*/traffic.json."""
-    import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
         try:
@@ -202,6 +202,20 @@ def committed_traffic(config: str, rows: int, tag: str):
         if d.get("config") == config and d.get("rows") == rows and tag in d.get("tags", {}):
             best = (os.path.relpath(f, ROOT), d["tags"][tag])
     return best
+
+
+def source_build_id() -> str:
+    """sha256 (16 hex) over the kernel and runtime sources the library is built from (trpo_amd/csrc,
+    include): the same id on the GPU box as here, with no git needed; profiles/*/traffic.json records
+    the id of the build its PMC pass measured."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "trpo_amd", "csrc", "*")) + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        if os.path.isfile(f) and not f.endswith((".o", ".so")):
+            h.update(os.path.relpath(f, ROOT).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def fvp_flops_per_row(widths) -> float:
@@ -366,6 +380,26 @@ def fvp_tags_per_call(prof):
     return tags, calls
 
 
+def comm_block(eng, world, rank, rehearsal, dist):
+    """The line's proof of what carried the all-reduces: the engine's transport, the RCCL communicator's
+    rank count, and every rank's HIP device and PCI bus id (gathered over torch.distributed).  Outside a
+    rehearsal, two ranks on one device end the run: that would not be a measurement of N GPUs."""
+    ci = eng.comm_info()
+    mine = {"rank": rank, "device": ci["device"], "pci_bus_id": ci["pci_bus_id"], "comm_rank": ci["comm_rank"],
+            "comm_device": ci["comm_device"]}
+    ranks = [mine]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    buses = [r["pci_bus_id"] for r in ranks]
+    if len(set(buses)) != len(buses) and not rehearsal:
+        raise SystemExit(f"ranks share a device outside --rehearsal: {buses}")
+    if ci["transport"] == "rccl" and ci["comm_count"] != world:
+        raise SystemExit(f"RCCL communicator has {ci['comm_count']} ranks, world is {world}")
+    return {"transport": ci["transport"], "ranks": ci["comm_count"] if ci["transport"] == "rccl" else world,
+            "world": world, "distinct_devices": len(set(buses)), "per_rank": ranks}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -380,6 +414,9 @@ def main():
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks per node than GPUs (they share GPUs through a host all-reduce)")
     ap.add_argument("--profile-out", default="", help="write the per-tag HIP-event profile here (JSON)")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="at one rank, still create a (one-rank) RCCL communicator: every all-reduce runs "
+                         "through RCCL, and the comm block records it")
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
@@ -413,6 +450,8 @@ def main():
 
     def comm_setup(eng):
         if world <= 1:
+            if args.rccl_world1:
+                eng.comm_init(eng.comm_unique_id(), 0, 1)
             return
         if rehearsal:
             # ranks share a GPU (RCCL refuses duplicate devices): all-reduce through gloo on the host
@@ -429,6 +468,7 @@ def main():
     wl = Workload(cfg, rank, world, gpu, dev)
     n, widths, N = wl.n, wl.widths, cfg["n"]
     eng = wl.engine(comm_setup)
+    comm = comm_block(eng, world, rank, rehearsal, dist)
     elapsed, last = timed_updates(eng, wl, args.steps, args.warmup, barrier)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -475,6 +515,7 @@ def main():
         by = tag_bytes(dom, widths, n)
         peak = tag_peak(dom, widths)
         achieved = fl / avg_s / 1e12
+        bound, _ = tag_roof(dom, widths, n)   # max(own bytes / HBM peak, FLOPs / MFMA peak)
         dom_prod = 6 if dom in ("fvp_chain", "fvp_fused") else prod   # chain / fused: exact bf16 x6 split
         peak_basis = (f"split MFMA: f16/bf16 dense peak 2.5 PF / {dom_prod} products" if tag_is_split(dom, widths)
                       else "f32 MFMA peak")
@@ -526,19 +567,31 @@ def main():
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"
                        if not rehearsal or world == 1 else
                        f"dp{world} on {ndev} GPU(s): rehearsal, ranks share GPUs, gloo host all-reduce"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
-                         "unit": "TFLOP/s", "frac": achieved / peak,
+            "roofline": {"bound": bound, "kernel": dom,
+                         "achieved": by / avg_s / 1e9 if bound == "hbm" else achieved,
+                         "peak": PEAK_HBM_GBS if bound == "hbm" else peak,
+                         "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
+                         "frac": (by / avg_s / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else achieved / peak,
                          "traffic": tr[1]["traffic_bytes"] if tr else None,
+                         "bound_basis": "the larger of the launch's own operand bytes / 8 TB/s and its FLOPs / "
+                                        "the split MFMA peak (bench.tag_roof)",
+                         "achieved_basis": ("algorithmic bytes of this launch (each activation operand read once, "
+                                            "each output written once, f32) / its average launch time"
+                                            if bound == "hbm" else
+                                            "SURVEY.md §8(d) algorithmic FLOPs of this kernel's share of the FVP "
+                                            "(4ab R-forward / 4ab R-backward / 4ab weight-R-gradient per state and "
+                                            "layer) / its average launch time"),
+                         "mfma_achieved_tflops": achieved, "mfma_peak_tflops": peak, "mfma_frac": achieved / peak,
                          "peak_basis": peak_basis,
-                         "achieved_basis": "SURVEY.md §8(d) algorithmic FLOPs of this kernel's share of the FVP "
-                                           "(4ab R-forward / 4ab R-backward / 4ab weight-R-gradient per state and "
-                                           "layer) / its average launch time",
                          "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt,
                          "own_traffic_bytes_per_launch": by,
                          "own_traffic_hbm_gbs": by / avg_s / 1e9,
                          "own_traffic_hbm_frac": by / avg_s / 1e9 / PEAK_HBM_GBS,
                          "hbm_gbs_at_traffic": tr[1]["traffic_bytes"] / avg_s / 1e9 if tr else None,
-                         "traffic_source": tr[0] if tr else None},
+                         "traffic_source": tr[0] if tr else None,
+                         "traffic_build": tr[1].get("build") if tr else None,
+                         "build": source_build_id(),
+                         "traffic_same_build": bool(tr and tr[1].get("build") == source_build_id())},
             "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
                                 "achieved_tflops": upd_flops * world / upd_s / 1e12,
                                 "roof_ms_per_update": upd_peak_s * 1e3,
@@ -551,6 +604,7 @@ def main():
                     "traffic_vs_algorithmic": fvp_moved / fvp_alg_bytes,
                     "tflops": fvp_flops_per_row(widths) * n / fvp_s / 1e12},
             "alt_arithmetic": alt,
+            "comm": comm,
             "last_update": {k: last[k] for k in ("cg_iters", "k", "reverted", "kl_after", "surr_after")},
             "cpu_baseline": None,
         }

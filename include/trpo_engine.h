@@ -99,6 +99,18 @@ int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world);
  * in place (e.g. torch.distributed over gloo).  Lets several ranks share one GPU in tests. */
 typedef int (*trpo_allreduce_cb)(void* host_buf, int64_t count, int dtype, void* ctx);
 int trpo_comm_set_host_allreduce(trpo_engine* e, trpo_allreduce_cb cb, void* ctx, int rank, int world);
+/* What carries this engine's all-reduces, for a launcher to verify (e.g. that N ranks of an RCCL
+ * communicator sit on N distinct devices).  transport: 0 none (one process), 1 RCCL, 2 host callback.
+ * comm_count / comm_rank / comm_device: ncclCommCount / ncclCommUserRank / ncclCommCuDevice of the RCCL
+ * communicator (-1 without one); device: the engine's HIP device; pci_bus_id: hipDeviceGetPCIBusId. */
+typedef struct trpo_comm_info_t {
+  int transport;
+  int rank, world;
+  int comm_count, comm_rank, comm_device;
+  int device;
+  char pci_bus_id[64];
+} trpo_comm_info_t;
+int trpo_comm_info(trpo_engine* e, trpo_comm_info_t* out);
 
 /* ---- parameters: SetFromFlat / GetFlat (utils.py:125-158) ---------------- */
 int trpo_set_flat(trpo_engine* e, const float* theta, int mem);

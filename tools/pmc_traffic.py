@@ -17,6 +17,7 @@ import csv
 import json
 import os
 import statistics
+import sys
 
 # tag -> (kernel-name substring, period, phase): the phase-th of every `period` dispatches
 # (kernel template arguments as rocprofv3 prints them; the last rowgemm3/wgrad3 argument is the
@@ -66,7 +67,9 @@ def main():
     a = ap.parse_args()
     fetch = load(os.path.join(a.pmc_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = load(os.path.join(a.pmc_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    res = {"config": a.config, "rows": a.rows, "source": a.pmc_dir,
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import source_build_id
+    res = {"config": a.config, "rows": a.rows, "source": a.pmc_dir, "build": source_build_id(),
            "method": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streams), write = WRITE_SIZE; "
                      "KiB -> bytes x 1024; mean over the matched launches", "tags": {}}
     todo = [(t, s, p, ph, False) for t, (s, p, ph) in SPECS.items()] + \

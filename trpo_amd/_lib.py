@@ -42,6 +42,11 @@ class RolloutParams(ctypes.Structure):
                 ("action_uniforms", c_void_p), ("max_episodes_per_env", c_int), ("mem", c_int)]
 
 
+class CommInfo(ctypes.Structure):
+    _fields_ = [("transport", c_int), ("rank", c_int), ("world", c_int), ("comm_count", c_int),
+                ("comm_rank", c_int), ("comm_device", c_int), ("device", c_int), ("pci_bus_id", ctypes.c_char * 64)]
+
+
 class FeedView(ctypes.Structure):
     _fields_ = [("n", c_int64), ("n_global", c_int64), ("obs_dim", c_int), ("n_actions", c_int),
                 ("states", c_void_p), ("ld_states", c_int), ("old_dist", c_void_p), ("ld_old", c_int),
@@ -63,6 +68,7 @@ SIGNATURES = {
     "trpo_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "trpo_comm_init": (c_int, [c_void_p, POINTER(c_uint8), c_int, c_int]),
     "trpo_comm_set_host_allreduce": (c_int, [c_void_p, ALLREDUCE_CB, c_void_p, c_int, c_int]),
+    "trpo_comm_info": (c_int, [c_void_p, ctypes.POINTER(CommInfo)]),
     "trpo_set_flat": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_get_flat": (c_int, [c_void_p, c_void_p, c_int]),
     "trpo_get_vector": (c_int, [c_void_p, c_int, c_void_p, c_int]),

@@ -1530,6 +1530,26 @@ int trpo_comm_set_host_allreduce(trpo_engine* e, trpo_allreduce_cb cb, void* ctx
   });
 }
 
+int trpo_comm_info(trpo_engine* e, trpo_comm_info_t* out) {
+  return guarded([&] {
+    REQUIRE(e && out, "NULL argument");
+    e->use();
+    trpo_comm_info_t ci{};
+    ci.transport = e->comm ? 1 : (e->host_ar ? 2 : 0);
+    ci.rank = e->rank;
+    ci.world = e->world;
+    ci.comm_count = ci.comm_rank = ci.comm_device = -1;
+    if (e->comm) {
+      NCCLCHECK(ncclCommCount(e->comm, &ci.comm_count));
+      NCCLCHECK(ncclCommUserRank(e->comm, &ci.comm_rank));
+      NCCLCHECK(ncclCommCuDevice(e->comm, &ci.comm_device));
+    }
+    ci.device = e->device;
+    HIPCHECK(hipDeviceGetPCIBusId(ci.pci_bus_id, (int)sizeof ci.pci_bus_id, e->device));
+    *out = ci;
+  });
+}
+
 int trpo_set_flat(trpo_engine* e, const float* theta, int mem) {
   return guarded([&] {
     REQUIRE(e && theta, "NULL argument");

@@ -143,6 +143,15 @@ class Engine:
         check(lib.trpo_comm_set_host_allreduce(self._h, self._host_ar, None, int(rank), int(world)),
               "trpo_comm_set_host_allreduce")
 
+    def comm_info(self) -> dict:
+        """What carries the all-reduces: transport ("none" / "rccl" / "host"), rank, world, the RCCL
+        communicator's rank count / user rank / device, this engine's HIP device and its PCI bus id."""
+        ci = _lib.CommInfo()
+        check(lib.trpo_comm_info(self._h, ctypes.byref(ci)), "trpo_comm_info")
+        return {"transport": ("none", "rccl", "host")[ci.transport], "rank": ci.rank, "world": ci.world,
+                "comm_count": ci.comm_count, "comm_rank": ci.comm_rank, "comm_device": ci.comm_device,
+                "device": ci.device, "pci_bus_id": ci.pci_bus_id.decode()}
+
     # ------------------------------------------------------------------ params
     def _out(self, out, dtype, n):
         if out is None:
