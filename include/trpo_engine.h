@@ -77,7 +77,7 @@ typedef struct trpo_update_stats {
 
 /* Build an engine for the categorical tanh-MLP policy of trpo_inksci.py:38-40
  * (hidden widths as a list; the reference is the depth-1 case {64}) with room
- * for `max_rows` states on GPU `device`.  n_actions <= 128 (the reference's softmax_classifier has
+ * for `max_rows` states on GPU `device`.  n_actions <= 128 for the update (trpo_act: <= 64; the reference's softmax_classifier has
  * no bound; a softmax row spans up to 4 x 32 lanes here). */
 int trpo_create(trpo_engine** out, int obs_dim, const int* hidden, int n_hidden, int n_actions,
                 int64_t max_rows, int device);
@@ -264,7 +264,9 @@ int trpo_set_baseline(trpo_engine* e, const double* baseline, int mem);
  * feed (all ranks), after the returns were computed; NaN when var(returns) == 0 */
 int trpo_explained_variance(trpo_engine* e, double* out);
 /* agent.act on n states [n][obs_dim] f32 (trpo_inksci.py:76-87): action_dist at the current
- * parameters and cat_sample against `uniforms` [n] (train = 1) or argmax (train = 0) */
+ * parameters and cat_sample against `uniforms` [n] (train = 1) or argmax (train = 0).
+ * n_actions <= 64 here (one wave per state): an engine created with 65..128 actions updates, but
+ * trpo_act returns an error for it (and trpo_rollout_cartpole needs exactly 2 actions). */
 int trpo_act(trpo_engine* e, const float* states, int64_t n, const double* uniforms, int train, int64_t* actions_out,
              float* dists_out, int mem);
 /* cat_sample(prob_nk) (utils.py:95-105) with the uniforms given: engine-free, current device */

@@ -14,6 +14,9 @@ n_global = 8M scaling through a row slice the oracle does evaluate:
                 running-max scales (norm-relative 1e-5)
 * arithmetic    f16x3 split vs the exact bf16x6 split on the same 8M batch (norm-relative 1e-5)
 * slice         3000 rows with n_global = 8M against the float64 oracle (SURVEY.md §8(d) bar)
+* whole update  the bench's full update at 8M (discount, standardise, pg, 10 CG, shs, line search) on its
+                own arithmetic (f16x3 + one-product low segment) vs three products everywhere and vs the
+                exact bf16x6 split: g, stepdir, fullstep, theta_new at 1e-5, CG count and k exact
 """
 import numpy as np
 import pytest
@@ -117,3 +120,57 @@ def test_c4_slice_at_n_global_8m_vs_oracle(gpu_available, big_batch):
     ref = O.fvp_undamped(big_batch["theta"].astype(np.float64), big_batch["X"][:n], v.astype(np.float64), SPEC,
                          n_global=N)
     assert_vec_close(hv, ref, REL, "Hv of a 3000-row slice at n_global = 8M")
+
+
+def _update_8m(b, opts):
+    """One whole update (discount + standardise + pg + 10 CG at residual_tol = 0 + shs + line search,
+    trpo_inksci.py:102-158) on the 8M batch with the given kernel options; returns the update's
+    vectors and scalars."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import (VEC_FULLSTEP, VEC_G, VEC_STEPDIR, VEC_THETA, get_option, set_option)
+    saved = {k: get_option(k) for k in opts}
+    for k, v in opts.items():
+        set_option(k, v)
+    try:
+        e = Engine(SPEC.obs_dim, SPEC.hidden, SPEC.n_actions, max_rows=N)
+        e.set_flat(b["theta"])
+        e.set_batch(b["X"], b["actions"], None, b["old"], n_global=N)
+        e.set_rewards(b["rewards"], b["starts"])
+        st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0, compute_advantages=True))
+        out = {"g": e.get_vector(VEC_G), "stepdir": e.get_vector(VEC_STEPDIR), "fullstep": e.get_vector(VEC_FULLSTEP),
+               "theta": e.get_vector(VEC_THETA), "stats": st}
+        e.close()
+    finally:
+        for k, v in saved.items():
+            set_option(k, v)
+    return out
+
+
+@pytest.fixture(scope="module")
+def updates_8m(big_batch, hv_f16):
+    rng = np.random.default_rng(5)
+    big_batch["rewards"] = rng.random(N)
+    big_batch["starts"] = (np.arange(N) % 200 == 0).astype(np.uint8)   # CartPole-v0 path length cap
+    return {"default": _update_8m(big_batch, {}),
+            "low_seg=0": _update_8m(big_batch, {"low_seg": 0}),
+            "bf16x6": _update_8m(big_batch, {"split_f16": 0})}
+
+
+@pytest.mark.parametrize("variant", ["low_seg=0", "bf16x6"])
+def test_c4_8m_whole_update_arithmetic(gpu_available, updates_8m, variant):
+    """The bench's headline update at its full size on the arithmetic the number is measured with
+    (f16x3 split + one-product low segment) against (a) three products everywhere and (b) the exact
+    bf16 hi+mid+lo split (6 products): g, stepdir, fullstep, theta_new at 1e-5; shs and the losses at
+    1e-5 relative; the CG iteration count and the line-search k exactly (trpo_inksci.py:146-158)."""
+    a, b = updates_8m["default"], updates_8m[variant]
+    sa, sb = a["stats"], b["stats"]
+    assert sa["cg_iters"] == sb["cg_iters"] == 10
+    assert sa["k"] == sb["k"] and sa["reverted"] == sb["reverted"]
+    for key in ("g", "stepdir", "fullstep", "theta"):
+        print(f"{variant} {key}: rel L2 {rel_l2(a[key], b[key]):.2e}")
+        assert_vec_close(a[key], b[key], REL, f"{key}: default vs {variant} at 8M")
+    assert sa["shs"] == pytest.approx(sb["shs"], rel=REL)
+    assert sa["lm"] == pytest.approx(sb["lm"], rel=REL)
+    for key in ("surr_after", "ent_after"):
+        assert sa[key] == pytest.approx(sb[key], rel=REL)
+    assert sa["kl_after"] == pytest.approx(sb["kl_after"], rel=REL, abs=1e-9)

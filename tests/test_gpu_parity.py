@@ -442,6 +442,12 @@ def test_two_ranks_c4_dims_f16_split(gpu_available):
     run_mrank("--host-allreduce", "--graphs", "--dims", "c4", "--rows", "120000")
 
 
+def test_two_ranks_c5_dims_f16_split(gpu_available):
+    """The same at C5 layer shapes (obs 376, 1024x1024, 17 actions: BASELINE configs[4], which the
+    reference quotes on 8 GPUs), 40k rows over two ranks (trpo_inksci.py:56-70,147)."""
+    run_mrank("--host-allreduce", "--dims", "c5", "--rows", "40000")
+
+
 def _graph_sequence(eng, d, n_small):
     """A fixed sequence of updates exercising graph capture, replay and re-keying: repeated
     updates from theta_0, consecutive updates, a cg_iters change, a batch-size change, an
@@ -610,6 +616,10 @@ def test_many_actions_vs_oracle(gpu_available, obs, hidden, A, n):
     r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
     assert st["k"] == r.k
     assert_vec_close(e.get_flat(), r.theta_new, REL, f"theta A={A}")
+    if A > 64:
+        # the update takes up to 128 actions; acting (one wave per state) stops at 64 and says so
+        with pytest.raises(RuntimeError, match="n_actions must be <= 64"):
+            e.act(dd["X"][:4], train=False)
     e.close()
 
 
@@ -647,6 +657,15 @@ def test_saturated_softmax_fvp_vs_oracle(gpu_available, scale, low_seg):
         hv = eng.fvp(v, 0.0)
         ref = O.fvp_undamped(theta.astype(np.float64), d["X"], v.astype(np.float64), spec)
         assert_vec_close(hv, ref, REL, "Hv")
+        # element-level parity per parameter block (each W_l and b_l against its own scale, so a small
+        # block -- the biases, the head -- is not judged against the largest block's magnitude): the
+        # one-product segment's 2^-11 relative error on its own terms must not surface in any block
+        off = 0
+        for l, (Wl, bl) in enumerate(O.unflatten(ref.copy(), spec)):
+            for name, blk in (("W", Wl), ("b", bl)):
+                sz = blk.size
+                assert_vec_close(hv[off:off + sz], ref[off:off + sz], REL, f"Hv block {name}{l}")
+                off += sz
         st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
         r = O.trpo_update(theta.astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], old),
                           spec, np.float64, 10, 0.0)
@@ -682,3 +701,23 @@ def test_path_switch_after_prepare_rewrites_e(gpu_available):
         e.close()
     finally:
         set_option("tail", saved)
+
+
+def test_flatgrad_of_gvp_is_the_fvp(gpu_available):
+    """The reference's spelling of the FVP node, ``self.fvp = flatgrad(gvp, var_list)`` with ``gvp`` the
+    tangent-dotted gradient of KL_firstfixed (trpo_inksci.py:56-70), and its damped closure
+    ``fisher_vector_product(p) = session.run(fvp) + 0.1 p`` (:124-126): through the utils surface against
+    the fixture's undamped Hv, and as the operator the device CG consumes."""
+    from trpo_amd.utils import FisherVectorProduct, KLFirstFixedGVP, conjugate_gradient, flatgrad
+    d = golden("update_c3.npz")
+    eng, spec = make_engine(d)
+    fvp = flatgrad(KLFirstFixedGVP(eng))
+    assert isinstance(fvp, FisherVectorProduct) and fvp.damping == 0.0
+    v = d["v"].astype(np.float32)
+    assert_vec_close(fvp(v), d["hv"], REL, "flatgrad(gvp)(v)")
+    fisher_vector_product = fvp.damped(0.1)
+    assert_vec_close(fisher_vector_product(v), d["hv"] + 0.1 * v, REL, "flatgrad(gvp)(v) + 0.1 v")
+    stepdir = conjugate_gradient(fisher_vector_product, -d["g"].astype(np.float32), int(d["cg_iters"]),
+                                 float(d["residual_tol"]))
+    assert_vec_close(stepdir, d["stepdir"], REL, "CG over the flatgrad(gvp) operator")
+    eng.close()

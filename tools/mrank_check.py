@@ -1,11 +1,12 @@
 """Several ranks on the visible GPU(s): the engine's multi-rank update vs a single-rank engine.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 \
-        tools/mrank_check.py [--host-allreduce] [--dims c3|c4] [--rows N] [--graphs]
+        tools/mrank_check.py [--host-allreduce] [--dims c3|c4|c5] [--rows N] [--graphs]
 
 --host-allreduce  ranks share a GPU (RCCL refuses duplicate devices): the engine's all-reduces run
                   through its stream-ordered host transport, summed by gloo on the host
 --dims c4         obs 128, 256x256, 18 actions: the wide layers take the f16-split MFMA row GEMMs
+--dims c5         obs 376, 1024x1024, 17 actions (BASELINE configs[4]'s layer shapes)
 --graphs          also replay the update as a captured hipGraph (all-reduces inside it) and require
                   every replay to be bitwise identical to the eager update
 Checks: ranks bitwise identical; Hv and theta within 1e-5 of one rank holding all rows; same k.
@@ -18,7 +19,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-DIMS = {"c3": (128, [64, 64], 18), "c4": (128, [256, 256], 18)}
+DIMS = {"c3": (128, [64, 64], 18), "c4": (128, [256, 256], 18), "c5": (376, [1024, 1024], 17)}
 
 
 def main():

@@ -53,6 +53,9 @@ int main(int argc, char** argv) {
     sa.job[1] = SplitJob{W + K * N, W3 + (size_t)2 * N * K, K, N, N, K, amW1};
     launch_split_b(sa, nullptr, 0);
   }
+  uint16_t* W3b = dalloc<uint16_t>((size_t)2 * 2 * N * K);   // k-blocked copies for the planes path
+  launch_block_planes(W3, 2, N, K, W3b, 0);
+  launch_block_planes(W3 + (size_t)2 * N * K, 2, N, K, W3b + (size_t)2 * N * K, 0);
   uint16_t *RHh = dalloc<uint16_t>((size_t)Mp * K), *RHl = dalloc<uint16_t>((size_t)Mp * K);
   uint16_t *Hh = dalloc<uint16_t>((size_t)Mp * K), *Hl = dalloc<uint16_t>((size_t)Mp * K);
   uint16_t *Dh = dalloc<uint16_t>((size_t)Mp * K), *Dl = dalloc<uint16_t>((size_t)Mp * K);
@@ -79,9 +82,11 @@ int main(int argc, char** argv) {
     g.seg[0] = GemmSeg{RH, W, K, N, cs == 2 ? 128 : (cs >= 5 ? 64 : K), W3, K, N * K, amRH, amW0};
     g.seg[1] = GemmSeg{A1, W + K * N, K, N, K, W3 + (size_t)2 * N * K, K, N * K, am1, amW1};
     if (planes) {
-      g.seg[0].Ah = RHh; g.seg[0].Al = RHl; g.seg[0].ldp = K; g.seg[0].eAp = es + 0;
-      g.seg[1].Ah = low ? Dh : Hh; g.seg[1].Al = low ? Dl : Hl; g.seg[1].ldp = K;
+      g.seg[0].Ah = RHh; g.seg[0].Al = RHl; g.seg[0].ldp = K; g.seg[0].mpad = (int)Mp; g.seg[0].eAp = es + 0;
+      g.seg[0].Bb = W3b;
+      g.seg[1].Ah = low ? Dh : Hh; g.seg[1].Al = low ? Dl : Hl; g.seg[1].ldp = K; g.seg[1].mpad = (int)Mp;
       g.seg[1].eAp = es + (low ? 2 : 1);
+      g.seg[1].Bb = W3b + (size_t)2 * N * K;
     }
     g.epi = (cs == 1 || cs == 5) ? RowEpi::kRBwd : ((cs == 3 || cs == 4) ? RowEpi::kTanh : RowEpi::kRHidden);
     g.ea.bias = bias; g.ea.H = Haux; g.ea.E = E; g.ea.RH = RH2; g.ea.ldo = N;

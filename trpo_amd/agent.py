@@ -29,8 +29,8 @@ import numpy as np
 
 from .engine import Engine, UpdateParams
 from .vf import VF
-from .utils import (EngineLoss, FisherVectorProduct, GetFlat, SetFromFlat, SurrogateLoss,
-                    conjugate_gradient, flatgrad, linesearch)
+from .utils import (EngineLoss, GetFlat, KLFirstFixedGVP, SetFromFlat, SurrogateLoss, conjugate_gradient,
+                    flatgrad, linesearch)
 
 CONFIG = {"max_steps": 1000, "episodes_per_roll": 1000, "gamma": 0.95, "cg_damping": 0.1,
           "max_kl": 0.01}   # trpo_inksci.py:17
@@ -99,6 +99,7 @@ class TRPOAgent:
         self.gf = GetFlat(self.session)                          # trpo_inksci.py:71
         self.sff = SetFromFlat(self.session)                     # :72
         self.pg = flatgrad(SurrogateLoss(self.engine))           # :54
+        self.fvp = flatgrad(KLFirstFixedGVP(self.engine))        # :56-70 (flatgrad(gvp))
         self.sff(xavier_theta(obs_dim, hidden, n_actions, self.session.init_rng) if theta is None else theta)
         self.train = True                                        # :28
         self.end_count = 0                                       # :29
@@ -126,7 +127,7 @@ class TRPOAgent:
         b = self.feed(paths_or_batch, n_global)
         if "rewards" in b:
             self.engine.compute_advantages(self.config["gamma"])      # :102-117
-        fisher_vector_product = FisherVectorProduct(self.engine, self.config["cg_damping"])   # :124-126
+        fisher_vector_product = self.fvp.damped(self.config["cg_damping"])                   # :124-126
         loss = EngineLoss(self.engine)                                                        # :127-129
         thprev = self.gf()                                                     # :144
         g = self.pg()                                                          # :146

@@ -38,6 +38,7 @@ using namespace trpo_abi;
 
 struct trpo_engine {
   int device = 0;
+  int num_cus = 256;               // compute units of `device` (hipDeviceAttributeMultiprocessorCount)
   hipStream_t stream = nullptr;
   // policy shape
   int L = 0;                       // layers
@@ -229,6 +230,7 @@ struct trpo_engine {
     for (int i = 0; i < nh; ++i) REQUIRE(hidden[i] > 0, "hidden widths must be positive");
     device = dev;
     use();
+    HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     w.push_back(obs);
     for (int i = 0; i < nh; ++i) w.push_back(hidden[i]);
@@ -1123,7 +1125,8 @@ struct trpo_engine {
     fa.ngroups = (int)((n + rb - 1) / rb);
     // one persistent workgroup per CU (8 waves) or two (4 waves), at most one per slab
     const int per_cu = variant == 2 ? 2 : 1;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)fa.ngroups, (int64_t)S, (int64_t)256 * per_cu}));
+    const int grid =
+        (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)fa.ngroups, (int64_t)S, (int64_t)num_cus * per_cu}));
     {
       Scope sp(this, "fvp_fused");
       launch_fvp_fused(fa, grid, variant, stream);
@@ -1702,6 +1705,12 @@ int trpo_standardize(trpo_engine* e, double* adv, int64_t n, int64_t n_global, f
         if (adv32_out) copy_out(adv32_out, d32, (size_t)n * sizeof(float), TRPO_MEM_HOST, s);
       }
       HIPCHECK(hipStreamSynchronize(s));
+      if (e) {
+        // the host all-reduce callbacks of the two sums ran during the sync: a failure there means the
+        // mean / std were rank-local, so it is this call's error (as fetch_scalars / copy_out report it)
+        e->har_pending = false;
+        e->check_har();
+      }
     } catch (...) {
       (void)hipStreamSynchronize(s);
       for (void* t : tmps) (void)hipFree(t);

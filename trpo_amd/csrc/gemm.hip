@@ -38,7 +38,7 @@ Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_in
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
                      env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
-                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14), env_int("TRPO_PL_WAVES", 8)};
+                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14)};
 
 namespace {
 

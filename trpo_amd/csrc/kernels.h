@@ -28,7 +28,6 @@ struct Options {
   int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves (default)
   int low_seg;     // f16 split GEMMs: a segment whose product scale sits >= low_seg binades below the other
                    // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
-  int pl_waves;    // pre-split row GEMM (plane.hip): 8 or 16 waves per 256 x 256 tile
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -62,12 +61,15 @@ struct GemmSeg {
   // set the power-of-two operand scales; NULL means "bounded by 1"
   const unsigned* amaxA = nullptr;
   const unsigned* amaxB = nullptr;
-  // f16 split, pre-split A (rowgemm_pl_kernel): A = (Ah + Al) * 2^-(*eAp), f16 planes [M][ldp] written
-  // once by their producer (ldp multiple of 64, zero for k >= K); Ah != NULL selects the planes path
+  // f16 split, pre-split operands (plane.hip): A = (Ah + Al) * 2^-(*eAp), f16 planes written once by their
+  // producer, k-blocked: element (r, k) at ((k / 32) * mpad + r) * 32 + k % 32, k padded to ldp (a multiple of
+  // 64) and rows to mpad (a multiple of 256), zero-filled; Bb = B's split planes k-blocked the same way,
+  // [2][ldk / 32][Npad][32] (plane = ldk * Npad elements).  Ah != NULL selects the planes path.
   const uint16_t* Ah = nullptr;
   const uint16_t* Al = nullptr;
-  int ldp = 0;
+  int ldp = 0, mpad = 0;
   const int* eAp = nullptr;
+  const uint16_t* Bb = nullptr;
 };
 
 enum class RowEpi : int {
@@ -125,10 +127,12 @@ struct RowGemmArgs {
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s);
 // the pre-split-plane form (plane.hip); launch_rowgemm dispatches to it when seg[0].Ah is set
 void launch_rowgemm_planes(const RowGemmArgs& a, hipStream_t s);
-// f32 A [M][lda] -> scaled f16 planes hi/lo [Mpad][ldp] (lo may be NULL: hi only); scale exponent
+// f32 A [M][lda] -> scaled f16 planes hi/lo, k-blocked (GemmSeg::Ah; lo may be NULL: hi only); scale exponent
 // f16_scale_exp(max |A|) from the running-max slot `amax` (NULL: |A| <= 1), written to *e_out
 void launch_split_planes(const float* A, int M, int Mpad, int K, int lda, uint16_t* hi, uint16_t* lo, int ldp,
                          const unsigned* amax, int* e_out, hipStream_t s);
+// k-block P planes [P][R][ld] (k contiguous) into [P][ld / 32][R][32] (GemmSeg::Bb)
+void launch_block_planes(const uint16_t* src, int P, int R, int ld, uint16_t* dst, hipStream_t s);
 // true when launch_rowgemm will take the split-bf16 path for this shape (the segments' B3 must be set)
 bool rowgemm_uses_split(int Npad, RowEpi epi);
 

@@ -109,6 +109,10 @@ class FisherVectorProduct:
     def __call__(self, p):
         return self.engine.fvp(p, self.damping)
 
+    def damped(self, damping: float) -> "FisherVectorProduct":
+        """``session.run(fvp) + damping * p`` (trpo_inksci.py:126) as an operator on the same engine."""
+        return FisherVectorProduct(self.engine, damping)
+
 
 def flatgrad(loss, var_list=None):
     """utils.py:119-122: the flat gradient node of ``loss`` w.r.t. the policy parameters."""
