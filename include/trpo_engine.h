@@ -201,7 +201,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * "low_seg" (f16 split GEMMs with two K-segments: a segment whose running-max product scale lies at
  * least this many binades below the other's -- the O(eps) KL_ff plain-delta terms -- runs on one
  * f16 product instead of three; 4 more binades when the dominant segment has an operand without a
- * running max; 0 = off; default 14).
+ * running max; 0 = off; default 14), "planes" (1 = row GEMMs whose operands the engine keeps as
+ * pre-split k-blocked f16 hi/lo planes run the LDS-DMA plane kernel of plane.hip; bit-identical to
+ * the register-staged split; default 1).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

@@ -85,7 +85,7 @@ def test_every_documented_option_is_known():
     text = open(os.path.join(ROOT, "include", "trpo_engine.h")).read()
     block = text[text.index("kernel-variant switches"):text.index("int trpo_set_option")]
     names = set(re.findall(r'"([a-z_0-9]+)"', block))
-    assert {"split_mfma", "split_f16", "chain", "graphs", "split_min_k", "low_seg"} <= names
+    assert {"split_mfma", "split_f16", "chain", "graphs", "split_min_k", "low_seg", "planes"} <= names
     for n in names:
         get_option(n)
     assert get_option("split_f16") == 1

@@ -286,6 +286,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
     {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
     {"low_seg": 0}, {"low_seg": 0, "chain": 0},               # every split segment on three products
+    {"planes": 0},                                            # register-staged split instead of the plane kernel
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -293,7 +294,8 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain", "split_f16", "split_min_k", "fused", "low_seg")}
+                                           "split_wg", "chain", "split_f16", "split_min_k", "fused", "low_seg",
+                                           "planes")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -550,8 +552,39 @@ def test_update_bench_dims_vs_oracle(gpu_available, obs, hidden, A, n):
     eng.close()
 
 
+@pytest.mark.parametrize("obs,hidden,A,n", [(128, [256, 256], 18, 3001), (376, [1024, 1024], 17, 1200),
+                                            (64, [512, 256], 18, 255)], ids=["c4_dims", "c5_dims", "k64_lt_tile"])
+def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n):
+    """Layer 0's row GEMMs (forward and R-forward) on the pre-split k-blocked X planes and the LDS-DMA
+    plane kernel (option planes, plane.hip) give bit-identical FVP, gradient and update to the
+    register-staged split of the same f16 arithmetic (ragged row tiles, K = 64 .. 384)."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    d = O.synthetic_batch(spec, n, seed=13)
+    v = np.random.RandomState(14).standard_normal(spec.n_params).astype(np.float32)
+    saved = get_option("planes")
+    out = {}
+    try:
+        for mode in (0, 1):
+            set_option("planes", mode)
+            eng = Engine(obs, hidden, A, max_rows=n + 300)
+            eng.set_flat(d["theta"])
+            eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+            hv, g = eng.fvp(v, 0.0), eng.policy_grad()
+            st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out[mode] = (hv, g, eng.get_flat(), st)
+            eng.close()
+    finally:
+        set_option("planes", saved)
+    for i, what in enumerate(("Hv", "g", "theta")):
+        np.testing.assert_array_equal(out[0][i], out[1][i], err_msg=what)
+    for k in ("cg_iters", "k", "shs", "lm", "surr_after", "kl_after"):
+        assert out[0][3][k] == out[1][3][k], k
+
+
 @pytest.mark.parametrize("obs,hidden,A,n", [
-    (128, [256, 256], 18, 3001),       # C4 dims (the bench workload's layer shapes), ragged last tile
+    (128, [256, 256], 18, 3001),      # C4 dims (the bench workload's layer shapes), ragged last tile
     (37, [200, 192], 17, 777),         # hidden 192: three of the four waves' column blocks, 17 actions
     (9, [64, 160, 256], 32, 1500),     # depth 3, A = 32 (one full action tile)
     (128, [256], 20, 64),              # the reference's depth (one hidden layer), fewer rows than a split

@@ -105,6 +105,29 @@ struct trpo_engine {
     if (first && count > 0)
       HIPCHECK(hipMemsetAsync(first, 0, (size_t)count * kAmaxSlot * sizeof(unsigned), stream));
   }
+  // pre-split k-blocked f16 planes for the plane row GEMM (plane.hip): X's hi/lo planes, refreshed with X's
+  // running max whenever X changes (layout stride x_mpad = round256(n)), and blocked copies of layer 0's
+  // W / V weight planes, re-blocked from WF3 / WFt3 before each use
+  uint16_t *Xh = nullptr, *Xl = nullptr, *W0b = nullptr, *V0b = nullptr;
+  int* pl_e = nullptr;   // scale exponents published by the plane producers: [0] = X
+  int x_mpad = 0, x_ldp = 0;
+  bool x_planes = false;   // Xh/Xl hold the current X
+  bool planes_geom_l0() const {   // layer 0's row GEMMs fit the plane kernel
+    return L >= 2 && wp[1] % 256 == 0 && r16(wp[0]) % 64 == 0;
+  }
+  bool planes_l0() const {
+    return x_planes && g_options.planes != 0 && split_on() && rowgemm_uses_split(wp[1], RowEpi::kTanh);
+  }
+  // attach X's planes and the blocked copy (into `dst`) of the 2 weight planes at `w3` to a layer-0 segment
+  void attach_x_planes(GemmSeg& sg, const uint16_t* w3, uint16_t* dst) {
+    launch_block_planes(w3, 2, wp[1], r16(wp[0]), dst, stream);
+    sg.Ah = Xh;
+    sg.Al = Xl;
+    sg.ldp = x_ldp;
+    sg.mpad = x_mpad;
+    sg.eAp = pl_e;
+    sg.Bb = dst;
+  }
   uint16_t* tail_planes = nullptr;   // head planes of the fused FVP tail (tail.hip), [2][2][32][kTailK]
   // the fused last-layer tail: f16 split, last hidden width in (128, 256], 17..32 actions
   bool use_tail() const {
@@ -317,6 +340,15 @@ struct trpo_engine {
     if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
     // allocated last: the big activation buffers keep the placement the kernels were tuned on
     stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
+    if (f16 && planes_geom_l0()) {
+      x_ldp = (wp[0] + 63) / 64 * 64;
+      const size_t xp = (size_t)((cap + 255) / 256 * 256) * x_ldp;
+      Xh = dalloc<uint16_t>(xp);
+      Xl = dalloc<uint16_t>(xp);
+      W0b = dalloc<uint16_t>(2 * plane3_f(0));
+      V0b = dalloc<uint16_t>(2 * plane3_f(0));
+      pl_e = dalloc<int>(8);
+    }
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
     setup_chain();
@@ -704,6 +736,7 @@ struct trpo_engine {
       seg3(a.seg[0], wf3[l], plane3_f(l), 0, wp[l]);
       a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
       a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
+      if (l == 0 && planes_l0()) attach_x_planes(a.seg[0], wf3[0], W0b);
       a.ea.bias = th + offb[l];
       a.ea.ldo = wp[l + 1];
       if (l < L - 1) {
@@ -747,6 +780,13 @@ struct trpo_engine {
     if (!f16) return;
     am_reset(am_x(), 1);
     launch_amax(X, n, w[0], wp[0], am_x(), stream);
+    x_planes = false;
+    if (Xh && g_options.planes != 0 && n > 0) {
+      x_mpad = (int)((n + 255) / 256 * 256);
+      Scope sp(this, "split_x");
+      launch_split_planes(X, (int)n, x_mpad, w[0], wp[0], Xh, Xl, x_ldp, am_x(), pl_e, stream);
+      x_planes = true;
+    }
     check_launch();
   }
 
@@ -896,6 +936,7 @@ struct trpo_engine {
         seg3(a.seg[0], WF3[l], plane3_f(l), 1, wp[l]);
         a.seg[0].amaxA = am_x();
         a.seg[0].amaxB = am_v(0);
+        if (planes_l0()) attach_x_planes(a.seg[0], WF3[0] + 3 * plane3_f(0), V0b);
       } else {
         a.nseg = 2;
         a.seg[0] = GemmSeg{RH[l], WF[l], wp[l], wp[l + 1], wp[l]};
@@ -2236,6 +2277,7 @@ static int* option_slot(const std::string& k) {
   if (k == "tail") return &g_options.tail;
   if (k == "fused") return &g_options.fused;
   if (k == "low_seg") return &g_options.low_seg;
+  if (k == "planes") return &g_options.planes;
   throw ArgError("unknown option " + k);
 }
 

@@ -38,7 +38,7 @@ Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_in
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
                      env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
-                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14)};
+                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14), env_int("TRPO_PLANES", 1)};
 
 namespace {
 
@@ -1464,7 +1464,9 @@ void launch_split_b(const SplitArgs& a, const int* skip, hipStream_t s) {
 
 void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
-  if (a.seg[0].Ah && !epi_is_head((int)a.epi)) {   // pre-split A planes (plane.hip)
+  // pre-split k-blocked A and B planes attached (plane.hip), where the register path would take the split
+  if (a.seg[0].Ah && g_options.planes != 0 && a.f16 && rowgemm_uses_split(a.Npad, a.epi) && !small_k_row(a) &&
+      a.Npad % 256 == 0) {
     launch_rowgemm_planes(a, s);
     return;
   }

@@ -28,6 +28,8 @@ struct Options {
   int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves (default)
   int low_seg;     // f16 split GEMMs: a segment whose product scale sits >= low_seg binades below the other
                    // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
+  int planes;      // engine: row GEMMs whose operands have pre-split k-blocked f16 planes take the LDS-DMA
+                   // plane kernel (plane.hip): 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
