@@ -203,7 +203,10 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * f16 product instead of three; 4 more binades when the dominant segment has an operand without a
  * running max; 0 = off; default 14), "planes" (1 = row GEMMs whose operands the engine keeps as
  * pre-split k-blocked f16 hi/lo planes run the LDS-DMA plane kernel of plane.hip; bit-identical to
- * the register-staged split; default 1).
+ * the register-staged split; default 1), "e16" (1 = the tanh'' terms E_l that the per-layer R-backward
+ * row GEMMs read are stored as the 16-bit high and low halves of each f32 word; the R-backward reads
+ * both halves (the f32 value, bit for bit) or, when the E RH term's running-max product scale lies
+ * low_seg + 3 binades below the main term's, the high halves alone; default 0: at C4 the test does not fire and the two 16-bit loads cost more than one f32 load).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

@@ -287,6 +287,8 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
     {"low_seg": 0}, {"low_seg": 0, "chain": 0},               # every split segment on three products
     {"planes": 0},                                            # register-staged split instead of the plane kernel
+    {"e16": 1, "rbwd0": 0}, {"e16": 1, "chain": 0, "rbwd0": 0},  # E_l as 16-bit high / low planes
+    {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -295,7 +297,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
                                            "split_wg", "chain", "split_f16", "split_min_k", "fused", "low_seg",
-                                           "planes")}
+                                           "planes", "e16", "rbwd0")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -564,6 +566,8 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
     d = O.synthetic_batch(spec, n, seed=13)
     v = np.random.RandomState(14).standard_normal(spec.n_params).astype(np.float32)
     saved = get_option("planes")
+    saved_r0 = get_option("rbwd0")
+    set_option("rbwd0", 0)   # the fused layer-1 R-backward needs X's planes: compare the row GEMMs alone
     out = {}
     try:
         for mode in (0, 1):
@@ -577,6 +581,7 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
             eng.close()
     finally:
         set_option("planes", saved)
+        set_option("rbwd0", saved_r0)
     for i, what in enumerate(("Hv", "g", "theta")):
         np.testing.assert_array_equal(out[0][i], out[1][i], err_msg=what)
     for k in ("cg_iters", "k", "shs", "lm", "surr_after", "kl_after"):
@@ -754,3 +759,102 @@ def test_flatgrad_of_gvp_is_the_fvp(gpu_available):
                                  float(d["residual_tol"]))
     assert_vec_close(stepdir, d["stepdir"], REL, "CG over the flatgrad(gvp) operator")
     eng.close()
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [(128, [256, 256], 18, 3001), (37, [200, 264, 144], 5, 1337),
+                                            (128, [256, 256, 256], 18, 2000)], ids=["c4_dims", "odd_wide", "depth3"])
+def test_e16_planes_exact_and_truncated(gpu_available, obs, hidden, A, n):
+    """E_l (the tanh'' term of the R-backward, trpo_inksci.py:56-70 through SURVEY.md Appendix A) kept as
+    the 16-bit high / low halves of each f32 word (option e16, RowEpi::kRBwd16).  With low_seg = 0 the
+    R-backward reads both halves: FVP, gradient and update are bit-identical to f32 E.  With the default
+    binade test the high halves alone may be read; the results must stay on the float64 oracle at 1e-5,
+    and re-preparing after an e16 switch must give the same bits as a fresh engine."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    d = O.synthetic_batch(spec, n, seed=41)
+    v = np.random.RandomState(42).standard_normal(spec.n_params).astype(np.float32)
+    saved = {k: get_option(k) for k in ("e16", "low_seg", "rbwd0")}
+    set_option("rbwd0", 0)   # the fused layer-1 R-backward reads f32 E (use_e16 is off under it)
+
+    def run(e16, low_seg):
+        set_option("e16", e16)
+        set_option("low_seg", low_seg)
+        eng = Engine(obs, hidden, A, max_rows=n + 100)
+        eng.set_flat(d["theta"])
+        eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+        hv, g = eng.fvp(v, 0.0), eng.policy_grad()
+        st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+        th = eng.get_flat()
+        eng.close()
+        return hv, g, th, st
+
+    try:
+        a, b = run(0, 0), run(1, 0)
+        for i, what in enumerate(("Hv", "g", "theta")):
+            np.testing.assert_array_equal(a[i], b[i], err_msg=f"e16 exact {what}")
+        t = run(1, 14)
+        ref = O.fvp_undamped(d["theta"].astype(np.float64), d["X"], v.astype(np.float64), spec)
+        assert_vec_close(t[0], ref, REL, "Hv, e16 with the high-half test")
+        r = O.trpo_update(d["theta"].astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], d["old_dist"]),
+                          spec, np.float64, 10, 0.0)
+        assert t[3]["k"] == r.k
+        assert_vec_close(t[2], r.theta_new, REL, "theta, e16 with the high-half test")
+        # one engine switched between the forms after prepare() re-prepares (engine.cpp fvp(), prep_e16)
+        set_option("low_seg", 0)
+        set_option("e16", 1)
+        eng = Engine(obs, hidden, A, max_rows=n + 100)
+        eng.set_flat(d["theta"])
+        eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+        h1 = eng.fvp(v, 0.0)
+        set_option("e16", 0)
+        h0 = eng.fvp(v, 0.0)
+        eng.close()
+        np.testing.assert_array_equal(h1, b[0])
+        np.testing.assert_array_equal(h0, a[0])
+    finally:
+        for k, val in saved.items():
+            set_option(k, val)
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (128, [256, 256], 18, 3001),       # C4 dims, ragged last tile of the last split
+    (37, [192, 200], 17, 2500),        # obs 37 (X planes 64 wide), hidden 192 (two idle waves), K = 200
+    (128, [256], 18, 1500),            # one hidden layer: the policy gradient's backward only (FVP in the tail)
+    (64, [256, 256, 256], 20, 900),    # depth 3
+], ids=["c4_dims", "odd", "one_hidden", "depth3"])
+def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
+    """rbwd0.hip: layer 1's R-backward with layer 0's weight R-gradient in one launch (RD_0 never stored),
+    and the same for the policy gradient's DS_0 (trpo_inksci.py:54,56-70), against the per-layer kernels
+    (option rbwd0 = 0) and the float64 oracle: Hv, g and a whole update."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + obs)
+    th = dd["theta"].astype(np.float64)
+    v = np.random.RandomState(n).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(th, dd["X"], v.astype(np.float64), spec)
+    gref = O.policy_grad(th, dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
+    saved = get_option("rbwd0")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("rbwd0", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            hv, g = e.fvp(v, 0.0), e.policy_grad()
+            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out[mode] = (hv, g, st, e.get_flat())
+            e.close()
+    finally:
+        set_option("rbwd0", saved)
+    for mode in (1, 0):
+        hv, g, st, theta = out[mode]
+        assert_vec_close(hv, ref, REL, f"Hv rbwd0={mode}")
+        assert_vec_close(g, gref, REL, f"g rbwd0={mode}")
+        assert st["k"] == r.k
+        assert_vec_close(theta, r.theta_new, REL, f"theta rbwd0={mode}")
+    assert_vec_close(out[1][0], out[0][0], REL, "fused vs per-layer Hv")
+    assert_vec_close(out[1][1], out[0][1], REL, "fused vs per-layer g")

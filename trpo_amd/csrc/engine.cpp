@@ -101,6 +101,7 @@ struct trpo_engine {
   unsigned* am_ds(int l) const { return am(4, l); }
   unsigned* am_rh(int l) const { return am(5, l); }
   unsigned* am_rd(int l) const { return am(6, l); }
+  unsigned* am_e(int l) const { return am(7, l); }
   void am_reset(unsigned* first, int count) {
     if (first && count > 0)
       HIPCHECK(hipMemsetAsync(first, 0, (size_t)count * kAmaxSlot * sizeof(unsigned), stream));
@@ -116,8 +117,11 @@ struct trpo_engine {
     return L >= 2 && wp[1] % 256 == 0 && r16(wp[0]) % 64 == 0;
   }
   bool planes_l0() const {
-    return x_planes && g_options.planes != 0 && split_on() && rowgemm_uses_split(wp[1], RowEpi::kTanh);
+    return x_planes && planes_geom_l0() && g_options.planes != 0 && split_on() &&
+           rowgemm_uses_split(wp[1], RowEpi::kTanh);
   }
+  // X's planes also feed the fused layer-1 R-backward + layer-0 weight gradient (rbwd0.hip)
+  bool rbwd0_geom() const { return L >= 2 && rbwd0_eligible(wp[0], (wp[0] + 63) / 64 * 64, wp[1], wp[2]); }
   // attach X's planes and the blocked copy (into `dst`) of the 2 weight planes at `w3` to a layer-0 segment
   void attach_x_planes(GemmSeg& sg, const uint16_t* w3, uint16_t* dst) {
     launch_block_planes(w3, 2, wp[1], r16(wp[0]), dst, stream);
@@ -138,6 +142,13 @@ struct trpo_engine {
   // but the fused tail, which recomputes it (tail.hip)
   bool e_top_needed() const { return L < 2 || !use_tail() || use_fused() || use_chain(); }
   bool prep_e_top = true;    // prepare() wrote E_{L-2}
+  // E_l as 16-bit high/low planes (RowEpi::kRBwd16) wherever the per-layer R-backward row GEMMs read them:
+  // every path but the chain / one-launch FVP and the opt-in last-layer fusions, which read f32 E
+  bool use_e16() const {
+    return g_options.e16 != 0 && !use_chain() && !use_fused() && !fused_head && !head_bwd && !use_rbwd0();
+  }
+  bool prep_e16 = false;     // prepare() wrote E in that form
+  int64_t e16_lo(int l) const { return cap * wp[l + 1]; }   // u16 offset of E_l's low-half plane
   bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
   bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
@@ -154,6 +165,41 @@ struct trpo_engine {
   // whole FVP (R-forward, head, R-backward and weight gradients) in one launch (fused.hip): one or
   // two hidden layers of width <= 64, obs <= 128, <= 32 actions; reuses the chain's weight images
   bool use_fused() const { return g_options.fused != 0 && chain_otm > 0 && fused_fvp_eligible(L, w.data()); }
+  // layer 1's R-backward (and the policy gradient's backward into layer 0) fused with layer 0's weight
+  // gradient (rbwd0.hip): f16 split with X's planes, obs <= 128, first hidden width <= 256
+  bool use_rbwd0() const {
+    return g_options.rbwd0 != 0 && f16 && x_planes && rbwd0_geom() && g_options.planes != 0 && split_on() &&
+           rowgemm_uses_split(wp[1], RowEpi::kRBwd);
+  }
+  RBwd0Args rbwd0_args(const int* skip) const {
+    RBwd0Args a{};
+    a.rows = (int)n;
+    a.K = wp[2];
+    a.lda = wp[2];
+    a.N = w[1];
+    a.Npad = wp[1];
+    a.obs = w[0];
+    a.B0 = WB3[1];
+    a.B1 = WB3[1] + 3 * plane3_b(1);
+    a.ldk = r16(wp[2]);
+    a.plane = (int64_t)plane3_b(1);
+    a.am_b0 = am_w(1);
+    a.am_b1 = am_v(1);
+    a.H = H[1];
+    a.Xh = Xh;
+    a.Xl = Xl;
+    a.x_mpad = x_mpad;
+    a.x_ldp = x_ldp;
+    a.eX = pl_e;
+    a.splits = active_splits;
+    a.rows_per_split = rows_per_split;
+    a.slab = slab;
+    a.slab_stride = slab_stride;
+    a.off_w = offW[0];
+    a.off_b = offb[0];
+    a.skip = skip;
+    return a;
+  }
   bool use_chain() const {
     return chain_otm > 0 && (g_options.chain >= 2 || (g_options.chain == 1 && chain_otm <= 8));
   }
@@ -336,11 +382,11 @@ struct trpo_engine {
                  g_options.fused_head != 0;   // opt-in: slower than the split kernels at C4 (1 block/CU)
     head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
     f16 = g_options.split_f16 != 0;
-    amax = dalloc<unsigned>((size_t)(1 + 7 * kMaxLayers) * kAmaxSlot);
+    amax = dalloc<unsigned>((size_t)(1 + 8 * kMaxLayers) * kAmaxSlot);
     if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
     // allocated last: the big activation buffers keep the placement the kernels were tuned on
     stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
-    if (f16 && planes_geom_l0()) {
+    if (f16 && (planes_geom_l0() || rbwd0_geom())) {
       x_ldp = (wp[0] + 63) / 64 * 64;
       const size_t xp = (size_t)((cap + 255) / 256 * 256) * x_ldp;
       Xh = dalloc<uint16_t>(xp);
@@ -807,6 +853,8 @@ struct trpo_engine {
     // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
     // recomputes it from H and D_{L-1}.
     prep_e_top = e_top_needed();
+    prep_e16 = use_e16();
+    am_reset(am_e(0), L);
     for (int l = L - 1; l >= 1; --l) {
       const bool need_d = l > 1, need_e = l < L - 1 || prep_e_top;
       if (!need_d && !need_e) continue;
@@ -817,11 +865,15 @@ struct trpo_engine {
       a.seg[0].amaxA = am_d(l);
       a.seg[0].amaxB = am_w(l);
       // both: kPrepBwd ; E only (D_0): kPrepBwdE ; D only: kPgBwd, whose epilogue is DH (1-H^2)
-      a.epi = need_d ? (need_e ? RowEpi::kPrepBwd : RowEpi::kPgBwd) : RowEpi::kPrepBwdE;
+      // (E as 16-bit planes: kPrepBwd16 / kPrepBwdE16, with its running max for the R-backward's test)
+      a.epi = need_d ? (need_e ? (prep_e16 ? RowEpi::kPrepBwd16 : RowEpi::kPrepBwd) : RowEpi::kPgBwd)
+                     : (prep_e16 ? RowEpi::kPrepBwdE16 : RowEpi::kPrepBwdE);
       a.ea.H = H[l];
       a.ea.out0 = need_d ? D[l - 1] : E[l - 1];
-      a.ea.amax0 = need_d ? am_d(l - 1) : nullptr;
+      a.ea.amax0 = need_d ? am_d(l - 1) : (prep_e16 ? am_e(l - 1) : nullptr);
       a.ea.out1 = need_d && need_e ? E[l - 1] : nullptr;
+      a.ea.amax1 = need_d && need_e && prep_e16 ? am_e(l - 1) : nullptr;
+      a.ea.e16_lo = e16_lo(l - 1);
       a.ea.ldo = wp[l];
       char t[32];
       std::snprintf(t, sizeof t, "bwd_l%d", l);
@@ -876,7 +928,19 @@ struct trpo_engine {
     DS[L - 1] = DSL;
     for (int l = 0; l < L - 1; ++l) DS[l] = RD[l];
     am_reset(am_ds(0), L - 1);
+    const bool r0f = use_rbwd0();
     for (int l = L - 1; l >= 1; --l) {
+      if (l == 1 && r0f) {
+        // DS_0 stays in registers: X^T DS_0 and its column sums go straight to the slab (rbwd0.hip)
+        RBwd0Args a = rbwd0_args(nullptr);
+        a.nseg = 1;
+        a.A0 = DS[1];
+        a.am_a0 = am_ds(1);
+        Scope sp(this, "pg_bwd0_wg0");
+        launch_rbwd0(a, stream);
+        check_launch();
+        continue;
+      }
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{DS[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
@@ -894,7 +958,7 @@ struct trpo_engine {
       launch_rowgemm(a, stream);
       check_launch();
     }
-    for (int l = 0; l < L; ++l) {
+    for (int l = r0f ? 1 : 0; l < L; ++l) {
       char t[32];
       std::snprintf(t, sizeof t, "pg_wgrad_l%d", l);
       wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1], l == 0 ? am_x() : nullptr, am_ds(l)}, WSeg{}, 0,
@@ -905,7 +969,8 @@ struct trpo_engine {
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
   void fvp(const float* v, float* out, const int* skip) {
-    if (prepared && e_top_needed() && !prep_e_top) prepared = false;   // the path changed since prepare()
+    // the path changed since prepare(): E_{L-2} needed but not written, or E in the other form
+    if (prepared && ((e_top_needed() && !prep_e_top) || prep_e16 != use_e16())) prepared = false;
     prepare();
     if (use_fused()) {
       fvp_fused(v, out, skip);
@@ -951,7 +1016,9 @@ struct trpo_engine {
       a.ea.bias = v + offb[l];
       a.ea.ldo = wp[l + 1];
       if (l < L - 1) {
-        a.epi = RowEpi::kRHidden;
+        // the fused tail is the only reader of RH_{L-1}: it gets the pre-activation and applies (1-H^2)
+        // itself, so H_{L-1} is read once per FVP instead of twice (its max bounds max |RH_{L-1}|)
+        a.epi = (tail && l == L - 2) ? RowEpi::kRZ : RowEpi::kRHidden;
         a.ea.H = H[l + 1];
         a.ea.out0 = RH[l + 1];
         a.ea.amax0 = am_rh(l + 1);
@@ -1047,6 +1114,7 @@ struct trpo_engine {
       ta.apad = wp[l];
       ta.bpad = wp[l + 1];
       ta.RH = RH[l];
+      ta.rz = 1;
       ta.H = H[l];
       ta.P = Pm;
       ta.DL = D[l];
@@ -1077,8 +1145,24 @@ struct trpo_engine {
       check_launch();
     }
     const bool tail_fused = fused_head || head_bwd || tail;
+    // layer 1's R-backward fused with layer 0's weight gradient when layer 1 is not inside the tail
+    const bool r0f = use_rbwd0() && (tail_fused ? L - 2 : L - 1) >= 1;
     // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
     for (int l = tail_fused ? L - 2 : L - 1; l >= 1; --l) {
+      if (l == 1 && r0f) {
+        RBwd0Args a = rbwd0_args(skip);
+        a.nseg = 2;
+        a.A0 = RD[1];
+        a.A1 = D[1];
+        a.am_a0 = am_rd(1);
+        a.am_a1 = am_d(1);
+        a.E = E[0];
+        a.RH = RH[1];
+        Scope sp(this, "fvp_rbwd1_wg0");
+        launch_rbwd0(a, stream);
+        check_launch();
+        continue;
+      }
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 2;
       a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
@@ -1090,9 +1174,12 @@ struct trpo_engine {
       a.seg[1].amaxA = am_d(l);
       a.seg[1].amaxB = am_v(l);
       a.skip = skip;
-      a.epi = RowEpi::kRBwd;
+      a.epi = prep_e16 ? RowEpi::kRBwd16 : RowEpi::kRBwd;
       a.ea.H = H[l];
       a.ea.E = E[l - 1];
+      a.ea.e16_lo = e16_lo(l - 1);
+      a.ea.amaxE = am_e(l - 1);
+      a.ea.amaxRH = am_rh(l);
       a.ea.RH = RH[l];
       a.ea.out0 = RD[l - 1];
       a.ea.amax0 = am_rd(l - 1);
@@ -1104,7 +1191,7 @@ struct trpo_engine {
       check_launch();
     }
     // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
-    for (int l = 0; l < (tail_fused ? L - 1 : L); ++l) {
+    for (int l = r0f ? 1 : 0; l < (tail_fused ? L - 1 : L); ++l) {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
       if (l == 0)
@@ -2278,6 +2365,8 @@ static int* option_slot(const std::string& k) {
   if (k == "fused") return &g_options.fused;
   if (k == "low_seg") return &g_options.low_seg;
   if (k == "planes") return &g_options.planes;
+  if (k == "e16") return &g_options.e16;
+  if (k == "rbwd0") return &g_options.rbwd0;
   throw ArgError("unknown option " + k);
 }
 

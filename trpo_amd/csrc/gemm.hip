@@ -38,7 +38,8 @@ Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_in
                      env_int("TRPO_HEAD_BWD", 0), env_int("TRPO_NARROW_PF", 1), env_int("TRPO_SPLIT_MFMA", 5),
                      env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
-                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14), env_int("TRPO_PLANES", 1)};
+                     env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14), env_int("TRPO_PLANES", 1),
+                     env_int("TRPO_E16", 0), env_int("TRPO_RBWD0", 1)};
 
 namespace {
 
@@ -1473,6 +1474,10 @@ void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
   switch (a.epi) {
     case RowEpi::kTanh: launch_row_epi<(int)RowEpi::kTanh>(a, s); break;
     case RowEpi::kRHidden: launch_row_epi<(int)RowEpi::kRHidden>(a, s); break;
+    case RowEpi::kRZ: launch_row_epi<(int)RowEpi::kRZ>(a, s); break;
+    case RowEpi::kPrepBwd16: launch_row_epi<(int)RowEpi::kPrepBwd16>(a, s); break;
+    case RowEpi::kPrepBwdE16: launch_row_epi<(int)RowEpi::kPrepBwdE16>(a, s); break;
+    case RowEpi::kRBwd16: launch_row_epi<(int)RowEpi::kRBwd16>(a, s); break;
     case RowEpi::kPrepBwd: launch_row_epi<(int)RowEpi::kPrepBwd>(a, s); break;
     case RowEpi::kPgBwd: launch_row_epi<(int)RowEpi::kPgBwd>(a, s); break;
     case RowEpi::kPrepBwdE: launch_row_epi<(int)RowEpi::kPrepBwdE>(a, s); break;

@@ -30,6 +30,10 @@ struct Options {
                    // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
   int planes;      // engine: row GEMMs whose operands have pre-split k-blocked f16 planes take the LDS-DMA
                    // plane kernel (plane.hip): 0 off, 1 on
+  int e16;         // engine: the tanh'' terms E_l read by per-layer R-backward row GEMMs are kept as 16-bit
+                   // high/low planes (RowEpi::kRBwd16): 0 off (f32), 1 on
+  int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
+                   // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -87,7 +91,18 @@ enum class RowEpi : int {
   kReluBwd = 9,   // out = acc * (H > 0), H = the ReLU output    (VF backward)
   kPrepBwdE = 10, // E = -2 acc H only                           (KL_ff plain backward into the first
                   //                                              hidden layer: D_0 has no reader)
+  kRZ = 11,       // RZ = acc + bias                             (R-forward pre-activation of the last
+                  //                                              hidden layer: the fused tail applies
+                  //                                              (1-H^2) as it loads H, so H is read once)
+  // E as two 16-bit planes (RowEpiArgs::e16_lo): the high and the low half of each f32 word, so a
+  // reader of both halves gets the f32 value bit for bit and a reader of the high half alone gets E
+  // truncated to 8 significant bits (the E RH term is O(eps) against the R-backward's main term)
+  kPrepBwd16 = 12,   // kPrepBwd with E (out1) as 16-bit planes
+  kPrepBwdE16 = 13,  // kPrepBwdE with E (out0) as 16-bit planes; running max |E| into amax0
+  kRBwd16 = 14,      // kRBwd with E as 16-bit planes; the low half is skipped when amaxE/amaxRH put the
+                     // E RH term >= low_seg + 3 binades below the main term's product scale
 };
+constexpr bool epi_e16(int e) { return e >= (int)RowEpi::kPrepBwd16 && e <= (int)RowEpi::kRBwd16; }
 // the row-wise softmax heads (one output row per 32-lane wave half, up to kMaxHeadTiles 32-column tiles)
 constexpr int kMaxHeadTiles = 4;
 constexpr bool epi_is_head(int e) { return e >= (int)RowEpi::kPrepHead && e <= (int)RowEpi::kRHead; }
@@ -113,6 +128,11 @@ struct RowEpiArgs {
   unsigned* amax0 = nullptr;
   unsigned* amax1 = nullptr;
   unsigned* amax2 = nullptr;
+  // 16-bit E planes (kPrepBwd16 / kPrepBwdE16 / kRBwd16): E's buffer holds the high halves at [0, .) and
+  // the low halves at e16_lo (uint16 elements) onward, both [M][ldo]
+  int64_t e16_lo = 0;
+  const unsigned* amaxE = nullptr;    // kRBwd16: running max |E| and |RH| (the high-half-only test)
+  const unsigned* amaxRH = nullptr;
 };
 
 struct RowGemmArgs {
@@ -436,8 +456,9 @@ namespace trpo {
 constexpr int kTailK = 256;   // max hidden width of the tail (head planes are [2][2][32][kTailK])
 struct TailArgs {
   int rows, a, b, apad, bpad;
-  const float* RH;            // [rows][apad]  R{h} of the last hidden layer
+  const float* RH;            // [rows][apad]  R{h} of the last hidden layer, or with rz its pre-activation RZ
   const float* H;             // [rows][apad]  its tanh activations
+  int rz = 0;                 // 1: RH holds RZ (kRZ); R{h} = (1-H^2) RZ is formed on load (same f32 ops as kRHidden)
   const float* P;             // [rows][bpad]  softmax at theta
   const float* DL;            // [rows][bpad]  KL_ff plain logit delta D_{L-1}
   const float* c;             // [b]           tangent bias of the last layer
@@ -463,6 +484,44 @@ struct TailPackArgs {
   uint16_t* out;              // [2][2][32][kTailK]
 };
 bool tail_eligible(int apad, int bpad);   // (128, kTailK] multiple of 32; bpad in (16, 32]
+
+// ---------------------------------------------------------------------------
+// R-backward into the first hidden layer fused with layer 0's weight R-gradient (rbwd0.hip).
+// Per 128-row tile of a split-K slab (trpo_inksci.py:56-70):
+//   RD_0  = ([RD_1 | D_1] [W_1^T ; V_1^T]) (1 - H_1^2) + E_0 RH_1      (kept in registers, never stored)
+//   slab += X^T RD_0 ;  bias += colsum RD_0                            (Hv's W_0 / b_0 blocks)
+// With nseg = 1, no E and no RH it is the policy gradient's DS_0 = (DS_1 W_1^T)(1 - H_1^2) and X^T DS_0
+// (trpo_inksci.py:54).  Hidden width <= 256 (wave w owns output columns [32w, 32w + 32)), obs <= 128 on
+// X's pre-split k-blocked f16 planes; products on the scaled f16 hi+lo split.
+// ---------------------------------------------------------------------------
+struct RBwd0Args {
+  int rows;                 // rows of this rank's shard
+  int K, lda;               // per-segment K (the layer-1 output width) and A's leading dimension
+  int N, Npad;              // layer-1 input width (RD_0's columns), padded (<= 256, multiple of 32)
+  int obs;                  // X's real columns (<= 128)
+  int nseg;                 // 2: [RD_1 | D_1] ; 1: DS_1 alone
+  const float* A0;          // [rows][lda] RD_1 (or DS_1)
+  const float* A1;          // [rows][lda] D_1
+  const uint16_t* B0;       // f16 hi/lo planes of W_1^T: [2][Npad][ldk] (plane stride `plane`)
+  const uint16_t* B1;       // ... of V_1^T
+  int ldk;
+  int64_t plane;
+  const unsigned *am_a0, *am_b0, *am_a1, *am_b1;   // running-max slots of the segment operands
+  const float* H;           // [rows][Npad] H_1
+  const float* E;           // [rows][Npad] E_0 (NULL: no E RH term)
+  const float* RH;          // [rows][Npad] RH_1
+  const uint16_t* Xh;       // X's k-blocked f16 planes (GemmSeg::Ah layout), scale 2^(*eX)
+  const uint16_t* Xl;
+  int x_mpad, x_ldp;
+  const int* eX;
+  int splits, rows_per_split;
+  float* slab;
+  int64_t slab_stride, off_w, off_b;
+  const int* skip;
+  int low_seg = 0;          // set at launch
+};
+bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
+void launch_rbwd0(const RBwd0Args& a, hipStream_t s);
 void launch_tail_pack(const TailPackArgs& p, hipStream_t s);
 void launch_fvp_tail(const TailArgs& a, hipStream_t s);
 }  // namespace trpo

@@ -1,0 +1,468 @@
+// R-backward into the first hidden layer fused with layer 0's weight R-gradient (gfx950).
+//
+// The per-layer FVP writes RD_0 = ([RD_1 | D_1] [W_1^T ; V_1^T]) (1 - H_1^2) + E_0 RH_1 to HBM in one row GEMM
+// and reads it back with X in a weight-gradient GEMM (X^T RD_0 and its column sums: Hv's W_0 / b_0 blocks,
+// trpo_inksci.py:56-70 through SURVEY.md Appendix A).  RD_0 has no other reader, so here it never leaves the
+// registers: per 128-row tile the row GEMM's accumulators become RD_0 in the epilogue and then, unchanged,
+// the B operand of the X^T RD_0 product, whose A operand (X^T) comes from an LDS image of X's pre-split
+// f16 planes.  Per row that removes RD_0's write and read (2 x 4 B per hidden column) and the second pass
+// over X.  The same kernel with one segment and no E term is the policy gradient's DS_0 = (DS_1 W_1^T)
+// (1 - H_1^2) with X^T DS_0 (trpo_inksci.py:54).
+//
+// Layout (32x32x16 f16 MFMA; lane l, r = l & 31, h = l >> 5; C: col = r, row = (i & 3) + 8 (i >> 2) + 4h):
+//   * 8 waves, one workgroup per split-K slab; wave w owns RD_0's columns [32w, 32w + 32) and all 128 rows of
+//     a tile (4 accumulator tiles), so its accumulator registers hold, for k-step s of the row-reduced
+//     product, rows 16s + 8(j >> 2) + 4h + (j & 3) of its 32 columns in registers 8(s & 1) + j of tile s >> 1:
+//     exactly a B operand (lane = column, 8 k-values) once split into f16 hi + lo.
+//   * X's tile image in LDS is [row][obs] per plane, 8-row x 32-column subtiles of 512 B with the 16-B chunks
+//     XOR-swizzled (cdna_hip_programming.md T10, image (a)); ds_read_b64_tr_b16 returns lane (obs m, h) the
+//     4 rows 16s + 8t + 4h .. +3 of column m, the matching A operand.  The image arrives by LDS-DMA
+//     (buffer_load ... lds) at the start of each tile, overlapped with the k-loop.
+//   * k-loop: the register-staged f16 split of rowgemm3_kernel (A split on the way to LDS, B from the
+//     engine's pre-split weight planes), BK = 16, two k-tiles of loads in flight.
+//   * Scales: the row GEMM's segments from their running-max slots; X from its planes' exponent; RD_0 per
+//     tile (workgroup max), the weight-gradient accumulator rescaled (exactly, by a power of two) whenever a
+//     tile needs a smaller exponent than the running one, and unscaled once at the end.
+#include "rowepi.h"
+#include <stdexcept>
+
+namespace trpo {
+namespace {
+
+#ifndef R0_ROWS
+#define R0_ROWS 128  // rows per tile
+#endif
+#ifndef R0_EC
+#define R0_EC 4      // epilogue chunk: accumulator registers per load batch
+#endif
+#ifndef R0_NW
+#define R0_NW 8      // waves per workgroup
+#endif
+constexpr int kR0Rows = R0_ROWS;              // rows per tile
+constexpr int kR0NW = R0_NW;                  // waves
+constexpr int kR0CT = 8 / kR0NW;              // 32-column tiles per wave: wave w owns RD_0 columns [32 CT w, ..)
+constexpr int kR0NT = kR0NW * 64;             // threads
+constexpr int kR0BK = 16;
+constexpr int kR0TM = kR0Rows / 32;           // accumulator row tiles per wave (all rows of the tile)
+constexpr int kR0XT = 4;                      // 32-column tiles of X (obs <= 128)
+constexpr int kR0APL = kR0Rows * kR0BK;       // u16 per A plane per stage
+constexpr int kR0BPL = 256 * kR0BK;           // u16 per B plane per stage
+constexpr int kR0STG = 2 * (kR0APL + kR0BPL); // u16 per stage (hi + lo planes of A and B)
+constexpr int kR0XPL = kR0Rows * 128;         // u16 per X plane image
+constexpr int kR0AI = kR0APL / 4 / kR0NT;     // f32x4 A staging items per thread
+constexpr int kR0BI = 2 * kR0BPL / 8 / kR0NT; // u16x8 B staging items per thread
+constexpr int kR0XP = 2 * kR0XPL * 2 / 1024;  // 1-KB X DMA pieces per tile (both planes)
+constexpr int kR0XD = kR0XP / kR0NW;          // ... per wave
+static_assert(kR0AI >= 1 && kR0APL % (4 * kR0NT) == 0 && kR0XP % kR0NW == 0, "rbwd0 tile shape");
+
+// byte offset of the 16-B chunk `ch` (8 obs) of `row` in an X plane image: 8-row x 32-column subtiles of
+// 512 B, chunks XOR-swizzled by row bits 2-3 (conflict-free ds_read_b64_tr_b16 of 4 rows x 16 columns)
+__device__ __forceinline__ int xoff(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// one 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane-linear destination at the wave-uniform LDS
+// byte address `lds`, per-lane source offset `voff` in the descriptor `rsrc` (M0 saved and restored)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds), "s"(0u));
+}
+
+#ifndef R0_PF
+#define R0_PF 2   // k-tiles of loads in flight: 1 or 2 (2: C4 fvp_rbwd1_wg0 14.5 -> 13.4 ms)
+#endif
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef short s8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+// x * 2^e -> f16 hi + lo for 8 values (round toward zero: x - hi exact, hi + lo within 2^-21 |x|)
+__device__ __forceinline__ void split8h(const float* x, float s, f16x8& hi, f16x8& lo) {
+  typedef __fp16 fp16x2 __attribute__((ext_vector_type(2)));
+  u32x4v H, L;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i] * s, b = x[2 * i + 1] * s;
+    const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, b);
+    const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], b - (float)hp[1]);
+    H[i] = __builtin_bit_cast(unsigned, hp);
+    L[i] = __builtin_bit_cast(unsigned, lp);
+  }
+  hi = __builtin_bit_cast(f16x8, H);
+  lo = __builtin_bit_cast(f16x8, L);
+}
+
+__device__ __forceinline__ f32x16 mfma3h(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl,
+                                         f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+}
+
+// NSEG = 2: FVP ([RD_1 | D_1], with the E RH term); NSEG = 1: policy gradient (DS_1, no E term)
+template <int NSEG>
+__global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
+  constexpr bool kE = NSEG == 2;
+  constexpr int TM = kR0TM, CT = kR0CT;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * kR0STG + 2 * kR0XPL];   // 48 + 64 KB
+  __shared__ float sMax[kR0NW];
+  if (A.skip && *A.skip) return;
+
+  const int tid0 = threadIdx.x;
+  const int r0 = blockIdx.x * A.rows_per_split;
+  const int r1 = min(A.rows, r0 + A.rows_per_split);
+  const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  const int Npad = A.Npad, lda = A.lda, K = A.K;
+  constexpr int kOob = 0x40000000;
+
+  // ---- scales (rowgemm3_kernel): per segment 2^eA, 2^eB; one product for a segment >= low_seg binades
+  //      below the other (the O(eps) D_1 V_1^T segment) ----
+  const int eA0 = amax_exp(A.am_a0), eB0 = amax_exp(A.am_b0);
+  const int eA1 = NSEG > 1 ? amax_exp(A.am_a1) : 0, eB1 = NSEG > 1 ? amax_exp(A.am_b1) : 0;
+  const int eP0 = eA0 + eB0, eP1 = eA1 + eB1;
+  bool one0 = false, one1 = false;
+  if (A.low_seg > 0 && NSEG > 1) {
+    one0 = __builtin_amdgcn_readfirstlane(eP0 - eP1 >= A.low_seg ? 1 : 0) != 0;
+    one1 = __builtin_amdgcn_readfirstlane(eP1 - eP0 >= A.low_seg ? 1 : 0) != 0;
+  }
+  const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
+  const int eX = __builtin_amdgcn_readfirstlane(*A.eX);
+
+  const int nk = (K + kR0BK - 1) / kR0BK;     // k-tiles per segment
+  const int ntiles = NSEG * nk;
+  const int bbytes = (int)(2 * A.plane * 2);
+
+  const unsigned xbytes = (unsigned)A.x_ldp * (unsigned)A.x_mpad * 2u;
+  const __amdgpu_buffer_rsrc_t rXh = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xh, 0, xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rXl = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xl, 0, xbytes, 0x00020000);
+  unsigned short* const sX = smem + 2 * kR0STG;
+  const unsigned lds_x = (unsigned)(uintptr_t)sX;
+
+  // lane-dependent values are recomputed per tile from an opaque copy of the thread id: hoisted out of
+  // the tile loop they stayed live across it (hundreds of registers of offsets, spilled)
+  auto lane_of = [&]() {
+    int t = tid0;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
+  f32x16 G[kR0XT][CT];   // X^T RD_0 for this wave's 64 columns; scaled by 2^(eX + Eacc)
+#pragma unroll
+  for (int i = 0; i < kR0XT; ++i)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) G[i][j] = f32x16{};
+  int Eacc = 1 << 20;   // sentinel: no nonzero tile yet
+  float bsum[CT] = {};  // colsum of RD_0 over this lane's rows, columns col0 + 32 tn + lr
+
+  for (int t0 = r0; t0 < r1; t0 += kR0Rows) {
+    const int Mt = min(kR0Rows, r1 - t0);
+    const int tid = lane_of(), lane = tid & 63, w = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int col0 = 32 * CT * w;
+    // X image DMA: wave w moves 1-KB pieces kR0XD w .. of the two 32-KB plane images; the source of lane
+    // `lane` in piece kb (row 0 of the tile; + 64 B per tile row)
+    auto xsrc = [&](int kb) {
+      const int o = (kb % (kR0XP / 2)) * 1024 + 16 * lane;   // byte offset in the plane image
+      const int row = 8 * (o >> 11) + ((o >> 6) & 7);
+      const int ch = 4 * ((o >> 9) & 3) + (((o >> 4) & 3) ^ ((row >> 2) & 3));
+      return (unsigned)(((ch >> 2) * A.x_mpad + row) * 32 + 8 * (ch & 3)) * 2u;
+    };
+    // X tile image (the previous tile's G phase is behind the loop-end barrier)
+#pragma unroll
+    for (int i = 0; i < kR0XD; ++i) {
+      const int kb = kR0XD * wv + i;   // wave-uniform: descriptor and LDS address in SGPRs
+      const int pl = kb / (kR0XP / 2);
+      dma16(pl ? rXl : rXh, xsrc(kb) + (unsigned)t0 * 64u,
+            lds_x + (unsigned)(pl * kR0XPL * 2 + (kb % (kR0XP / 2)) * 1024));
+    }
+
+    // ---- k-loop: acc = [A0 | A1] [B0 ; B1] on the f16 split ----
+    f32x16 acc[TM][CT];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{};
+    struct Stage {
+      f32x4 ra[kR0AI];
+      u16x8 rb[kR0BI];
+    };
+    auto gload = [&](Stage& st, int t) {
+      const bool s1 = t >= nk;
+      const float* Ap = s1 ? A.A1 : A.A0;
+      const int k0 = (s1 ? t - nk : t) * kR0BK;
+      const __amdgpu_buffer_rsrc_t rA =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(Ap + (size_t)t0 * lda), 0, Mt * lda * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? A.B1 : A.B0), 0, bbytes,
+                                                                          0x00020000);
+#pragma unroll
+      for (int i = 0; i < kR0AI; ++i) {
+        const int f = tid + i * kR0NT, r = f >> 2, kq = f & 3;
+        const int vo = (k0 + kR0BK > K && k0 + 4 * kq >= K) ? kOob : (r * lda + 4 * kq) * 4;
+        st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, k0 * 4, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < kR0BI; ++i) {
+        const int f = tid + i * kR0NT, p = f >> 9, rem = f & 511, n = rem >> 1, kh = rem & 1;
+        const int vo = n < Npad ? (int)((p * A.plane + (int64_t)n * A.ldk + 8 * kh) * 2) : kOob;
+        st.rb[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rB, vo, k0 * 2, 0));
+      }
+    };
+    auto sstore = [&](const Stage& st, int buf, bool s1) {
+      unsigned short* As = smem + buf * kR0STG;
+      unsigned short* Bs = As + 2 * kR0APL;
+      const float sa = s1 ? sA1 : sA0;
+#pragma unroll
+      for (int i = 0; i < kR0AI; ++i) {
+        const int f = tid + i * kR0NT, r = f >> 2, kq = f & 3;
+        u16x4 h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned short hh, ll;
+          split2h(st.ra[i][j] * sa, hh, ll);
+          h[j] = hh;
+          l[j] = ll;
+        }
+        unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
+        *reinterpret_cast<u16x4*>(dst) = h;
+        *reinterpret_cast<u16x4*>(dst + kR0APL) = l;
+      }
+#pragma unroll
+      for (int i = 0; i < kR0BI; ++i) {
+        const int f = tid + i * kR0NT, p = f >> 9, rem = f & 511;
+        *reinterpret_cast<u16x8*>(Bs + p * kR0BPL + swz16(rem >> 1, rem & 1)) = st.rb[i];
+      }
+    };
+    auto compute = [&](int buf, bool one) {
+      const unsigned short* As = smem + buf * kR0STG;
+      const unsigned short* Bs = As + 2 * kR0APL;
+      f16x8 bh[CT], bl[CT];
+#pragma unroll
+      for (int tn = 0; tn < CT; ++tn) {
+        const int bo = swz16(col0 + 32 * tn + lr, lh);
+        bh[tn] = *reinterpret_cast<const f16x8*>(Bs + bo);
+        bl[tn] = *reinterpret_cast<const f16x8*>(Bs + kR0BPL + bo);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int ao = swz16(32 * tm + lr, lh);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(As + ao);
+        if (one) {
+#pragma unroll
+          for (int tn = 0; tn < CT; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[tn], acc[tm][tn], 0, 0, 0);
+        } else {
+          const f16x8 al = *reinterpret_cast<const f16x8*>(As + kR0APL + ao);
+#pragma unroll
+          for (int tn = 0; tn < CT; ++tn) acc[tm][tn] = mfma3h(ah, al, bh[tn], bl[tn], acc[tm][tn]);
+        }
+      }
+    };
+    auto step = [&](int buf, int t) {
+      if (NSEG > 1 && t == nk) {
+        asm volatile("; segment switch" ::: "memory");   // a real branch (rowgemm3_kernel)
+        const float f = __builtin_ldexpf(1.0f, eP1 - eP0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < CT; ++j) acc[i][j] *= f;
+      }
+      compute(buf, t >= nk ? one1 : one0);
+    };
+    if (R0_PF == 1) {
+      Stage S;
+      gload(S, 0);
+      sstore(S, 0, false);
+      lds_barrier();
+      for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(S, t + 1);
+        step(t & 1, t);
+        if (t + 1 < ntiles) sstore(S, (t + 1) & 1, t + 1 >= nk);
+        lds_barrier();
+      }
+    } else {
+      Stage S0, S1;
+      gload(S0, 0);
+      gload(S1, ntiles > 1 ? 1 : 0);
+      sstore(S0, 0, false);
+      lds_barrier();
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
+        step(0, t);
+        sstore(S1, 1, t + 1 >= nk);
+        lds_barrier();
+        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+        step(1, t + 1);
+        if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
+        lds_barrier();
+      }
+      if (t < ntiles) step(0, t);
+    }
+    {
+      const float f = __builtin_ldexpf(1.0f, -(NSEG > 1 ? eP1 : eP0));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) acc[i][j] *= f;
+    }
+
+    // ---- epilogue: RD_0 = acc (1 - H^2) + E RH in place (rows past the split read 0: RD_0 = 0) ----
+    {
+      const int tb = Mt * Npad * 4;
+      auto mk = [&](const float* p) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (size_t)t0 * Npad), 0, tb, 0x00020000);
+      };
+      const __amdgpu_buffer_rsrc_t rH = mk(A.H), rE = mk(kE ? A.E : A.H), rRH = mk(kE ? A.RH : A.H);
+      // chunks of EC registers of one accumulator tile, the next chunk's loads in flight
+      constexpr int EC = R0_EC;
+      float pre[2][3][EC];
+      auto load_part = [&](int c, float (&d)[3][EC]) {
+        constexpr int PPT = 16 / EC;   // chunks per accumulator tile
+        const int tn = c % CT, tm = (c / CT) / PPT, hf = (c / CT) % PPT;
+        const int vo = col0 + 32 * tn < Npad ? ((4 * lh) * Npad + col0 + 32 * tn + lr) * 4 : kOob;
+#pragma unroll
+        for (int j = 0; j < EC; ++j) {
+          const int r = EC * hf + j;
+          const int so = (32 * tm + (r & 3) + 8 * (r >> 2)) * Npad * 4;
+          d[0][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rH, vo, so, 0));
+          if constexpr (kE) {
+            d[1][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, vo, so, 0));
+            d[2][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rRH, vo, so, 0));
+          } else {
+            d[1][j] = 0.0f;
+            d[2][j] = 0.0f;
+          }
+        }
+      };
+      constexpr int NC = (16 / EC) * TM * CT;
+      load_part(0, pre[0]);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (c + 1 < NC) load_part(c + 1, pre[(c + 1) & 1]);
+        const float (&op)[3][EC] = pre[c & 1];
+        const int tn = c % CT, tm = (c / CT) / (16 / EC), hf = (c / CT) % (16 / EC);
+#pragma unroll
+        for (int j = 0; j < EC; ++j) {
+          const int r = EC * hf + j;
+          acc[tm][tn][r] = fmaf(op[1][j], op[2][j], acc[tm][tn][r] * one_minus_sq(op[0][j]));
+        }
+        // no stores here to pin the loads: keep the scheduler from hoisting every chunk's loads
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    float mx = 0.0f;
+#pragma unroll
+    for (int tn = 0; tn < CT; ++tn)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          bsum[tn] += acc[tm][tn][r];
+          mx = fmaxf(mx, fabsf(acc[tm][tn][r]));
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if (lane == 0) sMax[w] = mx;
+    // the X image has landed (this wave's DMAs: vmcnt; every wave's: the barrier)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float mt = 0.0f;
+#pragma unroll
+    for (int u = 0; u < kR0NW; ++u) mt = fmaxf(mt, sMax[u]);
+    if (mt > 0.0f) {
+      // RD_0's tile exponent; the accumulator follows the smallest one so far (no f16 overflow)
+      const int et = f16_scale_exp(mt);
+      if (et < Eacc) {
+        if (Eacc != (1 << 20)) {
+          const float f = __builtin_ldexpf(1.0f, et - Eacc);
+#pragma unroll
+          for (int i = 0; i < kR0XT; ++i)
+#pragma unroll
+            for (int j = 0; j < CT; ++j) G[i][j] *= f;
+        }
+        Eacc = et;
+      }
+      const float sR = __builtin_ldexpf(1.0f, Eacc);
+      // ---- G += X^T RD_0: k-step s = rows 16s .. 16s + 15 of the tile ----
+      const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+      for (int s = 0; s < 2 * TM; ++s) {
+        f16x8 bh[CT], bl[CT];
+#pragma unroll
+        for (int tn = 0; tn < CT; ++tn) {
+          float vals[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vals[j] = acc[s >> 1][tn][8 * (s & 1) + j];
+          split8h(vals, sR, bh[tn], bl[tn]);
+        }
+#pragma unroll
+        for (int ot = 0; ot < kR0XT; ++ot) {
+          f16x8 xa[2];
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) {
+            s8 v;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const int row = 16 * s + 8 * t + 4 * (g4 >> 1) + q;
+              const int ch = 4 * ot + 2 * (g4 & 1) + (pp >> 1);
+              const s4 rr = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (__attribute__((address_space(3))) s4*)(sX + pl * kR0XPL + (xoff(row, ch) >> 1) + 4 * (pp & 1)));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[4 * t + e] = rr[e];
+            }
+            xa[pl] = __builtin_bit_cast(f16x8, v);
+          }
+#pragma unroll
+          for (int tn = 0; tn < CT; ++tn) G[ot][tn] = mfma3h(xa[0], xa[1], bh[tn], bl[tn], G[ot][tn]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();   // X image and staging buffers free for the next tile
+  }
+
+  // ---- this split's slab: W_0 block [obs][N] and the bias colsum ----
+  const int lane = tid0 & 63, lr = lane & 31, lh = lane >> 5, col0 = 32 * CT * (tid0 >> 6);
+  float* out = A.slab + (size_t)blockIdx.x * A.slab_stride;
+  const float fG = Eacc == (1 << 20) ? 0.0f : __builtin_ldexpf(1.0f, -(eX + Eacc));
+#pragma unroll
+  for (int tn = 0; tn < CT; ++tn) {
+    const int j = col0 + 32 * tn + lr;
+    if (j < A.N) {
+#pragma unroll
+      for (int ot = 0; ot < kR0XT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = 32 * ot + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (i < A.obs) out[A.off_w + (int64_t)i * A.N + j] = G[ot][tn][r] * fG;
+        }
+    }
+    const float bt = xadd_f<true>(bsum[tn]);   // the two lane halves' rows, same order on both
+    if (lh == 0 && j < A.N) out[A.off_b + j] = bt;
+  }
+}
+
+}  // namespace
+
+bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K) {
+  return obs_pad <= 128 && x_ldp <= 128 && hid_pad <= 256 && hid_pad % 32 == 0 && K >= 4 && K % 4 == 0;
+}
+
+void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
+  if (a.splits <= 0) return;
+  if (!rbwd0_eligible(a.obs, a.x_ldp, a.Npad, a.K) || a.obs > 128 || !a.Xh || !a.Xl || !a.eX || !a.H ||
+      (a.nseg > 1 && (!a.A1 || !a.B1)) || (a.E && !a.RH) || a.ldk < (a.K + 15) / 16 * 16 || a.lda < a.K)
+    throw std::runtime_error("rbwd0: unsupported shape or missing operand");
+  if ((int64_t)a.x_ldp * a.x_mpad * 2 >= (int64_t(1) << 32) || (int64_t)kR0Rows * a.lda * 4 >= (int64_t(1) << 31))
+    throw std::runtime_error("rbwd0: operand beyond the buffer-descriptor range");
+  if ((int64_t)a.splits * a.rows_per_split < a.rows) throw std::runtime_error("rbwd0: splits do not cover the rows");
+  if (a.nseg != 1 && a.nseg != 2) throw std::runtime_error("rbwd0: nseg must be 1 or 2");
+  if ((a.nseg == 2) != (a.E != nullptr)) throw std::runtime_error("rbwd0: the E RH term goes with two segments");
+  RBwd0Args b = a;
+  b.low_seg = g_options.low_seg;
+  if (a.nseg == 2) hipLaunchKernelGGL(rbwd0_kernel<2>, dim3(a.splits), dim3(kR0NT), 0, s, b);
+  else hipLaunchKernelGGL(rbwd0_kernel<1>, dim3(a.splits), dim3(kR0NT), 0, s, b);
+}
+
+}  // namespace trpo

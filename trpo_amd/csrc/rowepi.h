@@ -124,6 +124,8 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
     e.out0[idx] = real ? tanh_fast(v + e.bias[col]) : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kRHidden) {
     e.out0[idx] = real ? one_minus_sq(e.H[idx]) * (v + e.bias[col]) : 0.0f;
+  } else if constexpr (EPI == (int)RowEpi::kRZ) {
+    e.out0[idx] = real ? v + e.bias[col] : 0.0f;
   } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
     if (real) {
       const float h = e.H[idx];
@@ -146,6 +148,12 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
   }
 }
 
+// E from its 16-bit high / low planes (RowEpi::kRBwd16), bit for bit
+__device__ __forceinline__ float e16_load(const RowEpiArgs& e, size_t idx) {
+  const uint16_t* p = reinterpret_cast<const uint16_t*>(e.E);
+  return __builtin_bit_cast(float, ((unsigned)p[idx] << 16) | (unsigned)p[e.e16_lo + idx]);
+}
+
 // value part (loads + math) and store part of the element-wise epilogues.
 // No column predicate: padding columns (col >= N) have zero accumulators (zero
 // weight padding), zero bias and zero H/E/RH padding, so every formula below
@@ -158,12 +166,16 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
     o0 = tanh_fast(v + bv);
   } else if constexpr (EPI == (int)RowEpi::kRHidden) {
     o0 = one_minus_sq(e.H[idx]) * (v + bv);
-  } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
+  } else if constexpr (EPI == (int)RowEpi::kRZ) {
+    o0 = v + bv;
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16) {
     const float h = e.H[idx];
     o0 = v * one_minus_sq(h);
     o1 = -2.0f * v * h;
-  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPrepBwdE16) {
     o0 = -2.0f * v * e.H[idx];
+  } else if constexpr (EPI == (int)RowEpi::kRBwd16) {
+    o0 = fmaf(e16_load(e, idx), e.RH[idx], v * one_minus_sq(e.H[idx]));
   } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
     o0 = v * one_minus_sq(e.H[idx]);
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
@@ -176,9 +188,21 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
 }
 template <int EPI>
 __device__ __forceinline__ void epi_store(const RowEpiArgs& e, size_t idx, float o0, float o1) {
-  e.out0[idx] = o0;
-  if constexpr (EPI == (int)RowEpi::kPrepBwd) e.out1[idx] = o1;
+  auto st16 = [&](float* base, float v) {   // the two 16-bit halves of v into E's planes
+    uint16_t* p = reinterpret_cast<uint16_t*>(base);
+    const unsigned b = __builtin_bit_cast(unsigned, v);
+    p[idx] = (uint16_t)(b >> 16);
+    p[e.e16_lo + idx] = (uint16_t)(b & 0xffffu);
+  };
+  if constexpr (EPI == (int)RowEpi::kPrepBwdE16) {
+    st16(e.out0, o0);
+  } else {
+    e.out0[idx] = o0;
+    if constexpr (EPI == (int)RowEpi::kPrepBwd) e.out1[idx] = o1;
+    if constexpr (EPI == (int)RowEpi::kPrepBwd16) st16(e.out1, o1);
+  }
 }
+
 
 // ---------------------------------------------------------------------------
 // row-wise softmax-head epilogues.  The row's columns live on the 32 lanes of one wave half, TN
@@ -342,13 +366,175 @@ __device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
   nt = swz - mt * ntn;
 }
 
+// Full-width tile of the element-wise epilogues: every epilogue operand goes through a per-block buffer
+// descriptor (base = row m0, num_records = the rows this tile owns), so a load/store is one buffer op with
+// a lane-constant voffset and a per-row SGPR soffset; rows past M fall outside the descriptor (loads read
+// 0, stores are dropped) -- no per-element predicate, no 64-bit address math, and all 16 loads of a chunk
+// stay in flight.  ETRUNC (kRBwd16 only): read the high halves of E alone.
+template <int WM, int WN, int TM, int TN, int EPI, bool ETRUNC>
+__device__ __forceinline__ void row_epi_full(const RowGemmArgs& args, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
+                                             int wn, int lr, int lh, float& mx0, float& mx1) {
+  constexpr int BM = WM * TM * 32;
+  const int M = args.M;
+  const RowEpiArgs& e = args.ea;
+  const int ldo = e.ldo;
+  const int Mt = M - m0 < BM ? M - m0 : BM;
+  const int tile_bytes = Mt * ldo * 4;
+  auto mk = [&](const float* ptr) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
+  };
+  // E's 16-bit planes: the high halves from the buffer's base, the low halves e16_lo elements on
+  auto mk16 = [&](const float* ptr, bool lo) {
+    const uint16_t* p = reinterpret_cast<const uint16_t*>(ptr) + (lo ? e.e16_lo : 0) + (size_t)m0 * ldo;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, tile_bytes / 2, 0x00020000);
+  };
+  constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
+                          EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPgBwd ||
+                          EPI == (int)RowEpi::kRBwd || EPI == (int)RowEpi::kReluBwd || epi_e16(EPI);
+  constexpr bool kRB16 = EPI == (int)RowEpi::kRBwd16;
+  constexpr bool kRB = EPI == (int)RowEpi::kRBwd || kRB16;
+  constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16;
+  constexpr bool kPB = EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16;
+  constexpr bool kPE = EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPrepBwdE16;
+  // where E goes as 16-bit planes: out1 (kPrepBwd16) or out0 (kPrepBwdE16)
+  constexpr int kE16Out = EPI == (int)RowEpi::kPrepBwd16 ? 1 : (EPI == (int)RowEpi::kPrepBwdE16 ? 0 : -1);
+  // descriptors of operands an epilogue does not use alias out0 and are never touched
+  const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
+  const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
+  const __amdgpu_buffer_rsrc_t rE = mk((kRB && !kRB16) ? e.E : e.out0);
+  const __amdgpu_buffer_rsrc_t rEh = mk16(kRB16 ? e.E : e.out0, false);
+  const __amdgpu_buffer_rsrc_t rEl = mk16(kRB16 ? e.E : e.out0, kRB16);
+  const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
+  const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
+  const float* e16o = kE16Out == 1 ? e.out1 : e.out0;
+  const __amdgpu_buffer_rsrc_t rSh = mk16(e16o, false);
+  const __amdgpu_buffer_rsrc_t rSl = mk16(e16o, kE16Out >= 0);
+  const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  };
+  auto ld16 = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, vo >> 1, so >> 1, 0);
+  };
+  auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+  };
+  auto st16 = [&](float v, int vo, int so) {
+    const unsigned b = __builtin_bit_cast(unsigned, v);
+    // (the b16 buffer builtins take and return unsigned short: raw bits, no conversion)
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b >> 16), rSh, vo >> 1, so >> 1, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b & 0xffffu), rSl, vo >> 1, so >> 1, 0);
+  };
+  // Operand loads run one (tm, tn) chunk ahead of the chunk being computed and stored: the
+  // chunk's loads are issued before the previous chunk's stores in program order (hipcc cannot
+  // prove the descriptors disjoint, so it would not hoist them itself), which leaves one chunk
+  // of loads in flight behind every chunk of math instead of a full round trip per chunk.
+  constexpr int NL = kRB ? 3 : (kUsesH ? 1 : 0);
+  constexpr int NCH = TM * TN;
+  float pre[2][NL > 0 ? NL : 1][16];
+  auto load_chunk = [&](int c, float (&dst)[NL > 0 ? NL : 1][16]) {
+    if constexpr (NL > 0) {
+      const int tn = c / TM, tm = c % TM;
+      const int vo = vbase + tn * 128;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+        dst[0][r] = ld(rH, vo, so);
+        if constexpr (NL == 3) {
+          if constexpr (kRB16) {
+            const unsigned hi = ld16(rEh, vo, so) << 16;
+            dst[1][r] = __builtin_bit_cast(float, ETRUNC ? hi : (hi | ld16(rEl, vo, so)));
+          } else {
+            dst[1][r] = ld(rE, vo, so);
+          }
+          dst[2][r] = ld(rRH, vo, so);
+        }
+      }
+    }
+  };
+  if constexpr (TRPO_EPI_PIPE) load_chunk(0, pre[0]);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int tn = c / TM, tm = c % TM;
+    const int col = n0 + wn * TN * 32 + tn * 32 + lr;
+    float bv = 0.0f;
+    if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu ||
+                  EPI == (int)RowEpi::kRZ)
+      bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
+    const int vo = vbase + tn * 128;
+    if constexpr (TRPO_EPI_PIPE) {
+      if (c + 1 < NCH) load_chunk(c + 1, pre[(c + 1) & 1]);
+    } else {
+      load_chunk(c, pre[c & 1]);
+    }
+    const float (&op)[NL > 0 ? NL : 1][16] = pre[c & 1];
+    {
+      float o0[16], o1[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[tm][tn][r];
+        if constexpr (EPI == (int)RowEpi::kTanh) {
+          o0[r] = tanh_fast(v + bv);
+        } else if constexpr (EPI == (int)RowEpi::kRHidden) {
+          o0[r] = one_minus_sq(op[0][r]) * (v + bv);
+        } else if constexpr (EPI == (int)RowEpi::kRZ) {
+          o0[r] = v + bv;
+        } else if constexpr (kPB) {
+          const float h = op[0][r];
+          o0[r] = v * one_minus_sq(h);
+          o1[r] = -2.0f * v * h;
+        } else if constexpr (kPE) {
+          o0[r] = -2.0f * v * op[0][r];
+        } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
+          o0[r] = v * one_minus_sq(op[0][r]);
+        } else if constexpr (EPI == (int)RowEpi::kRelu) {
+          o0[r] = fmaxf(v + bv, 0.0f);
+        } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
+          o0[r] = op[0][r] > 0.0f ? v : 0.0f;
+        } else {
+          o0[r] = fmaf(op[1][r], op[2][r], v * one_minus_sq(op[0][r]));
+        }
+        // running max for the f16 operand scales (rows past M -- dropped stores -- hold 0 or,
+        // for kRHidden, the tangent bias: harmless in a max)
+        if constexpr (TRPO_EPI_TRACK && EPI != (int)RowEpi::kTanh && EPI != (int)RowEpi::kRelu &&
+                      EPI != (int)RowEpi::kReluBwd && EPI != (int)RowEpi::kPrepBwdE) {
+          mx0 = fmaxf(mx0, fabsf(o0[r]));
+          if constexpr (kPB) mx1 = fmaxf(mx1, fabsf(o1[r]));
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
+        if constexpr (kE16Out == 0) st16(o0[r], vo, so);
+        else st(o0[r], rO0, vo, so);
+        if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
+        if constexpr (kE16Out == 1) st16(o1[r], vo, so);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int amax_exp(const unsigned* amax);
+
+// kRBwd16: whether E's high halves alone are enough -- the E RH term's running-max product scale sits at
+// least low_seg + 3 binades below the main term's (segment 0, RD W^T): truncation to 8 significant bits
+// (2^-7 relative) then stays 2^-(low_seg - 4) below the dominant products, the one-product segment's bar
+// (rowgemm3_kernel).  Uniform over the launch.
+__device__ __forceinline__ bool e16_trunc_ok(const RowGemmArgs& args) {
+  const RowEpiArgs& e = args.ea;
+  if (args.low_seg <= 0 || !e.amaxE || !e.amaxRH || !args.seg[0].amaxA || !args.seg[0].amaxB) return false;
+  const int qE = amax_exp(e.amaxE) + amax_exp(e.amaxRH);
+  const int q0 = amax_exp(args.seg[0].amaxA) + amax_exp(args.seg[0].amaxB);
+  return __builtin_amdgcn_readfirstlane(qE - q0 >= args.low_seg + 3 ? 1 : 0) != 0;
+}
+
 // Fused epilogue of a row-GEMM tile.  The accumulator layout (col = lane&31,
 // row = (r&3) + 8(r>>2) + 4(lane>>5)) is the same for the f32 (32x32x2) and the
 // bf16 (32x32x16) MFMA, so both row-GEMM kernels share it.
 template <int WM, int WN, int TM, int TN, int EPI, bool EXT_RED = false>
 __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&acc)[TM][TN], int m0, int n0,
                                              int wm, int wn, int lr, int lh, float (*red)[16] = nullptr) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int BN = WN * TN * 32;
   const int M = args.M;
   const RowEpiArgs& e = args.ea;
   float mx0 = 0.0f, mx1 = 0.0f, mx2 = 0.0f;   // max |stored output| for the f16 operand scales
@@ -367,113 +553,11 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
   } else {
     const bool fulln = (n0 + BN <= args.Npad);
     if (fulln) {
-      // Full-width tile: every epilogue operand goes through a per-block buffer
-      // descriptor (base = row m0, num_records = the rows this tile owns), so a
-      // load/store is one buffer op with a lane-constant voffset and a per-row SGPR
-      // soffset; rows past M fall outside the descriptor (loads read 0, stores are
-      // dropped) -- no per-element predicate, no 64-bit address math, and all 16
-      // loads of a chunk stay in flight.
-      const int ldo = e.ldo;
-      const int Mt = M - m0 < BM ? M - m0 : BM;
-      const int tile_bytes = Mt * ldo * 4;
-      auto mk = [&](const float* ptr) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
-      };
-      constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
-                              EPI == (int)RowEpi::kPrepBwdE ||
-                              EPI == (int)RowEpi::kPgBwd || EPI == (int)RowEpi::kRBwd ||
-                              EPI == (int)RowEpi::kReluBwd;
-      constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
-      constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd;
-      // descriptors of operands an epilogue does not use alias out0 and are never touched
-      const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
-      const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
-      const __amdgpu_buffer_rsrc_t rE = mk(kRB ? e.E : e.out0);
-      const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
-      const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
-      const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
-      auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
-      };
-      auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
-      };
-      // Operand loads run one (tm, tn) chunk ahead of the chunk being computed and stored: the
-      // chunk's loads are issued before the previous chunk's stores in program order (hipcc cannot
-      // prove the descriptors disjoint, so it would not hoist them itself), which leaves one chunk
-      // of loads in flight behind every chunk of math instead of a full round trip per chunk.
-      constexpr int NL = kRB ? 3 : (kUsesH ? 1 : 0);
-      constexpr int NCH = TM * TN;
-      float pre[2][NL > 0 ? NL : 1][16];
-      auto load_chunk = [&](int c, float (&dst)[NL > 0 ? NL : 1][16]) {
-        if constexpr (NL > 0) {
-          const int tn = c / TM, tm = c % TM;
-          const int vo = vbase + tn * 128;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
-            dst[0][r] = ld(rH, vo, so);
-            if constexpr (NL == 3) {
-              dst[1][r] = ld(rE, vo, so);
-              dst[2][r] = ld(rRH, vo, so);
-            }
-          }
-        }
-      };
-      if constexpr (TRPO_EPI_PIPE) load_chunk(0, pre[0]);
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int tn = c / TM, tm = c % TM;
-        const int col = n0 + wn * TN * 32 + tn * 32 + lr;
-        float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu)
-          bv = e.bias[col < args.N ? col : 0] * (col < args.N ? 1.0f : 0.0f);
-        const int vo = vbase + tn * 128;
-        if constexpr (TRPO_EPI_PIPE) {
-          if (c + 1 < NCH) load_chunk(c + 1, pre[(c + 1) & 1]);
-        } else {
-          load_chunk(c, pre[c & 1]);
-        }
-        const float (&op)[NL > 0 ? NL : 1][16] = pre[c & 1];
-        {
-          float o0[16], o1[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = acc[tm][tn][r];
-            if constexpr (EPI == (int)RowEpi::kTanh) {
-              o0[r] = tanh_fast(v + bv);
-            } else if constexpr (EPI == (int)RowEpi::kRHidden) {
-              o0[r] = one_minus_sq(op[0][r]) * (v + bv);
-            } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
-              const float h = op[0][r];
-              o0[r] = v * one_minus_sq(h);
-              o1[r] = -2.0f * v * h;
-            } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
-              o0[r] = -2.0f * v * op[0][r];
-            } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
-              o0[r] = v * one_minus_sq(op[0][r]);
-            } else if constexpr (EPI == (int)RowEpi::kRelu) {
-              o0[r] = fmaxf(v + bv, 0.0f);
-            } else if constexpr (EPI == (int)RowEpi::kReluBwd) {
-              o0[r] = op[0][r] > 0.0f ? v : 0.0f;
-            } else {
-              o0[r] = fmaf(op[1][r], op[2][r], v * one_minus_sq(op[0][r]));
-            }
-            // running max for the f16 operand scales (rows past M -- dropped stores -- hold 0 or,
-            // for kRHidden, the tangent bias: harmless in a max)
-            if constexpr (TRPO_EPI_TRACK && EPI != (int)RowEpi::kTanh && EPI != (int)RowEpi::kRelu &&
-                          EPI != (int)RowEpi::kReluBwd && EPI != (int)RowEpi::kPrepBwdE) {
-              mx0 = fmaxf(mx0, fabsf(o0[r]));
-              if constexpr (EPI == (int)RowEpi::kPrepBwd) mx1 = fmaxf(mx1, fabsf(o1[r]));
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
-            st(o0[r], rO0, vo, so);
-            if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
-          }
-        }
+      if constexpr (EPI == (int)RowEpi::kRBwd16) {
+        if (e16_trunc_ok(args)) row_epi_full<WM, WN, TM, TN, EPI, true>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
+        else row_epi_full<WM, WN, TM, TN, EPI, false>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
+      } else {
+        row_epi_full<WM, WN, TM, TN, EPI, false>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
       }
     } else {
       // partial-width tile (odd layer widths): predicated path
@@ -484,7 +568,8 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
         const bool colv = col < args.Npad;
         const int colc = colv ? col : 0;
         float bv = 0.0f;
-        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu)
+        if constexpr (EPI == (int)RowEpi::kTanh || EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kRelu ||
+                      EPI == (int)RowEpi::kRZ)
           bv = e.bias[real ? col : 0];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)

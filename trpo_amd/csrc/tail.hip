@@ -197,6 +197,12 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
   for (int t0 = r0; t0 < r1; t0 += TR, par ^= 1) {
     float nRH[16], nH[16], nP[2], nD[2];
     if (t0 + TR < r1) load_c(t0 + TR, nRH, nH, nP, nD);
+    // RZ in, R{h} = (1 - H^2) RZ formed here: the R-forward that feeds the tail then never reads H
+    // (RowEpi::kRZ); the same f32 operations as its kRHidden epilogue, so R{h} is bit-identical
+    if (A.rz) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cRH[i] = omsq(cH[i]) * cRH[i];
+    }
 
     // ---- head R-forward partial over this wave's 32 columns: RZ = RH W + H V.  The tile's C layout
     //      (lane = column k, registers = rows m) goes to LDS as f16 planes [k][m], each lane storing
