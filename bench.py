@@ -108,6 +108,10 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return ab if l == 0 else 2 * ab
     if role == "fvp_rbwd":
         return 2 * ab
+    if role == "fvp_rbwdwg":        # rbwd0.hip: layer l's R-backward (2ab) + layer l-1's weight R-gradient
+        return 2 * ab + 2.0 * n * widths[l - 1] * widths[l]
+    if role == "pg_bwdwg":          # rbwd0.hip: the surr backward into layer l-1 + its weight gradient
+        return ab + 2.0 * n * widths[l - 1] * widths[l]
     if role == "fvp_tail":          # fused last layer: R-forward (2ab) + R-backward (2ab) + weight R-gradient (2ab)
         return 6 * ab
     if role == "fvp_head":          # R-forward (2ab) + R-backward (2ab) + wgrad (2ab) of the last layer
@@ -132,7 +136,7 @@ def tag_is_split(tag: str, widths) -> bool:
         return get_option("split_wg") != 0 and b > 128
     if role in ("fvp_head", "fvp_headbwd"):
         return False
-    if role == "fvp_tail":              # tail.hip: always the f16 hi+lo split (3 products)
+    if role in ("fvp_tail", "fvp_rbwdwg", "pg_bwdwg"):   # tail.hip / rbwd0.hip: always the f16 hi+lo split
         return True
     last = l == len(widths) - 2
     out = a if role in ("bwd", "pg_bwd", "fvp_rbwd") else b
@@ -161,14 +165,19 @@ def tag_bytes(tag: str, widths, n: int) -> float:
     w = widths
     cols = 0
     if role == "fvp_rfwd":
+        rz = l == L - 2 and tail_used(widths)               # kRZ: the tail applies (1-H^2), H_{l+1} not read
         if l == 0:
-            cols = w[0] + 2 * w[1]                          # X ; H1 (epilogue) ; RH1 out
+            cols = w[0] + (1 if rz else 2) * w[1]           # X ; H1 (epilogue) ; RH1 out
         elif l < L - 1:
-            cols = 2 * w[l] + 2 * w[l + 1]                  # RH_l, H_l ; H_{l+1} ; RH_{l+1} out
+            cols = 2 * w[l] + (1 if rz else 2) * w[l + 1]   # RH_l, H_l ; H_{l+1} ; RH_{l+1} (or RZ) out
         else:
             cols = 2 * w[l] + 2 * w[l + 1]                  # RH, H ; P ; RD_L out
     elif role == "fvp_rbwd":
         cols = 2 * w[l + 1] + 4 * w[l]                      # RD_l, D_l ; H_l, E, RH_l ; RD_{l-1} out
+    elif role == "fvp_rbwdwg":
+        cols = 2 * w[l + 1] + 3 * w[l] + w[l - 1]           # RD_l, D_l ; H_l, E, RH_l ; X (RD_{l-1} stays on chip)
+    elif role == "pg_bwdwg":
+        cols = w[l + 1] + w[l] + w[l - 1]                   # DS_l ; H_l ; X
     elif role == "fvp_tail":
         cols = 3 * w[l] + 2 * w[l + 1]                      # RH_l, H_l ; P, D_L ; RD_{l-1} out
     elif role == "fvp_wgrad":
@@ -182,6 +191,17 @@ def tag_bytes(tag: str, widths, n: int) -> float:
     elif role == "pg_wgrad":
         cols = w[l] + w[l + 1]
     return 4.0 * n * cols
+
+
+def tail_used(widths) -> bool:
+    """Whether the engine runs the fused last-layer tail (engine.cpp use_tail, tail.hip tail_eligible)."""
+    from trpo_amd._lib import get_option
+    pad = lambda v: (v + 3) // 4 * 4
+    L = len(widths) - 1
+    if L < 2 or not (get_option("tail") and get_option("split_f16") and get_option("split_mfma")):
+        return False
+    a, b = pad(widths[L - 1]), pad(widths[L])
+    return 128 < a <= 256 and a % 32 == 0 and 16 < b <= 32 and widths[L] <= 32
 
 
 def tag_roof(tag: str, widths, n: int):

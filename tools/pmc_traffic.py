@@ -23,15 +23,14 @@ import sys
 # (kernel template arguments as rocprofv3 prints them; the last rowgemm3/wgrad3 argument is the
 # plane count: 2 = the default f16 split)
 SPECS = {
-    "fvp_rfwd_l0": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 0),
-    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 1, 2, 2, 2>", 2, 1),
-    "fvp_rbwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 4, 2, 2, 2>", 1, 0),
+    "fvp_rfwd_l0": ("rowgemm_pl_kernel<1>", 1, 0),                          # X planes, kRHidden (plane.hip)
+    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 11, 2, 2, 2>", 1, 0),      # kRZ into the tail
+    "fvp_rbwdwg_l1": ("rbwd0_kernel<2>", 1, 0),                             # R-backward + X^T RD_0 (rbwd0.hip)
     "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
     "fvp_wgrad_l1": "wgrad3_kernel<4, 2, 2, 4, 2, 1, 2>",
-    "fvp_wgrad_l0": "wgrad3_kernel<2, 4, 2, 2, 2, 1, 2>",
 }
 
 

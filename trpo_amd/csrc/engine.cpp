@@ -936,7 +936,7 @@ struct trpo_engine {
         a.nseg = 1;
         a.A0 = DS[1];
         a.am_a0 = am_ds(1);
-        Scope sp(this, "pg_bwd0_wg0");
+        Scope sp(this, "pg_bwdwg_l1");
         launch_rbwd0(a, stream);
         check_launch();
         continue;
@@ -1158,7 +1158,7 @@ struct trpo_engine {
         a.am_a1 = am_d(1);
         a.E = E[0];
         a.RH = RH[1];
-        Scope sp(this, "fvp_rbwd1_wg0");
+        Scope sp(this, "fvp_rbwdwg_l1");
         launch_rbwd0(a, stream);
         check_launch();
         continue;

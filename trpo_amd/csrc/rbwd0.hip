@@ -20,11 +20,13 @@
 //     (buffer_load ... lds) at the start of each tile, overlapped with the k-loop.
 //   * k-loop: the register-staged f16 split of rowgemm3_kernel (A split on the way to LDS, B from the
 //     engine's pre-split weight planes), BK = 16, two k-tiles of loads in flight.
-//   * Scales: the row GEMM's segments from their running-max slots; X from its planes' exponent; RD_0 per
+//   * Scales: the row GEMM's two segments share one product scale (the smaller of their running-max ones,
+//     so one 3-product k-loop covers both); X from its planes' exponent; RD_0 per
 //     tile (workgroup max), the weight-gradient accumulator rescaled (exactly, by a power of two) whenever a
 //     tile needs a smaller exponent than the running one, and unscaled once at the end.
 #include "rowepi.h"
 #include <stdexcept>
+#include <type_traits>
 
 namespace trpo {
 namespace {
@@ -34,6 +36,9 @@ namespace {
 #endif
 #ifndef R0_EC
 #define R0_EC 4      // epilogue chunk: accumulator registers per load batch
+#endif
+#ifndef R0_PF
+#define R0_PF 4      // k-tiles of A / B loads in flight (register stages): 2 or 4
 #endif
 #ifndef R0_NW
 #define R0_NW 8      // waves per workgroup
@@ -53,6 +58,8 @@ constexpr int kR0AI = kR0APL / 4 / kR0NT;     // f32x4 A staging items per threa
 constexpr int kR0BI = 2 * kR0BPL / 8 / kR0NT; // u16x8 B staging items per thread
 constexpr int kR0XP = 2 * kR0XPL * 2 / 1024;  // 1-KB X DMA pieces per tile (both planes)
 constexpr int kR0XD = kR0XP / kR0NW;          // ... per wave
+constexpr int kR0LDSU = 2 * kR0STG + 2 * kR0XPL;   // u16: two staging buffers + the X image
+static_assert(kR0LDSU * 2 <= 160 * 1024, "rbwd0 LDS");
 static_assert(kR0AI >= 1 && kR0APL % (4 * kR0NT) == 0 && kR0XP % kR0NW == 0, "rbwd0 tile shape");
 
 // byte offset of the 16-B chunk `ch` (8 obs) of `row` in an X plane image: 8-row x 32-column subtiles of
@@ -71,8 +78,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff
                : "v"(voff), "s"(rsrc), "s"(lds), "s"(0u));
 }
 
-#ifndef R0_PF
-#define R0_PF 2   // k-tiles of loads in flight: 1 or 2 (2: C4 fvp_rbwd1_wg0 14.5 -> 13.4 ms)
+#ifndef R0_ABL
+#define R0_ABL 0   // timing ablations only (A/B builds): 1 no X^T RD_0 phase, 2 no epilogue loads, 3 no k-loop
 #endif
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef short s8 __attribute__((ext_vector_type(8)));
@@ -106,7 +113,7 @@ template <int NSEG>
 __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   constexpr bool kE = NSEG == 2;
   constexpr int TM = kR0TM, CT = kR0CT;
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * kR0STG + 2 * kR0XPL];   // 48 + 64 KB
+  __shared__ __attribute__((aligned(16))) unsigned short smem[kR0LDSU];
   __shared__ float sMax[kR0NW];
   if (A.skip && *A.skip) return;
 
@@ -117,17 +124,15 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   const int Npad = A.Npad, lda = A.lda, K = A.K;
   constexpr int kOob = 0x40000000;
 
-  // ---- scales (rowgemm3_kernel): per segment 2^eA, 2^eB; one product for a segment >= low_seg binades
-  //      below the other (the O(eps) D_1 V_1^T segment) ----
+  // ---- scales: both segments' products share one power-of-two scale 2^eP, the smaller of their
+  //      running-max product scales (rowgemm3_kernel's per-segment eA + eB): the dominant segment's A is
+  //      scaled as in rowgemm3_kernel, the other's below its own optimum (the O(eps) D_1 V_1^T segment
+  //      sits ~15 binades under, where 3 products keep it at 2^-11 of itself, 2^-26 of the dominant
+  //      products).  One k-loop over both segments, no accumulator rescale, never an f16 overflow. ----
   const int eA0 = amax_exp(A.am_a0), eB0 = amax_exp(A.am_b0);
   const int eA1 = NSEG > 1 ? amax_exp(A.am_a1) : 0, eB1 = NSEG > 1 ? amax_exp(A.am_b1) : 0;
-  const int eP0 = eA0 + eB0, eP1 = eA1 + eB1;
-  bool one0 = false, one1 = false;
-  if (A.low_seg > 0 && NSEG > 1) {
-    one0 = __builtin_amdgcn_readfirstlane(eP0 - eP1 >= A.low_seg ? 1 : 0) != 0;
-    one1 = __builtin_amdgcn_readfirstlane(eP1 - eP0 >= A.low_seg ? 1 : 0) != 0;
-  }
-  const float sA0 = __builtin_ldexpf(1.0f, eA0), sA1 = __builtin_ldexpf(1.0f, eA1);
+  const int eP = NSEG > 1 ? min(eA0 + eB0, eA1 + eB1) : eA0 + eB0;
+  const float sA0 = __builtin_ldexpf(1.0f, eP - eB0), sA1 = __builtin_ldexpf(1.0f, eP - eB1);
   const int eX = __builtin_amdgcn_readfirstlane(*A.eX);
 
   const int nk = (K + kR0BK - 1) / kR0BK;     // k-tiles per segment
@@ -168,14 +173,17 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       const int ch = 4 * ((o >> 9) & 3) + (((o >> 4) & 3) ^ ((row >> 2) & 3));
       return (unsigned)(((ch >> 2) * A.x_mpad + row) * 32 + 8 * (ch & 3)) * 2u;
     };
-    // X tile image (the previous tile's G phase is behind the loop-end barrier)
+    // X tile image (the previous tile's G phase is behind the loop-end barrier), overlapped with the k-loop
+    auto x_dma = [&]() {
 #pragma unroll
-    for (int i = 0; i < kR0XD; ++i) {
-      const int kb = kR0XD * wv + i;   // wave-uniform: descriptor and LDS address in SGPRs
-      const int pl = kb / (kR0XP / 2);
-      dma16(pl ? rXl : rXh, xsrc(kb) + (unsigned)t0 * 64u,
-            lds_x + (unsigned)(pl * kR0XPL * 2 + (kb % (kR0XP / 2)) * 1024));
-    }
+      for (int i = 0; i < kR0XD; ++i) {
+        const int kb = kR0XD * wv + i;   // wave-uniform: descriptor and LDS address in SGPRs
+        const int pl = kb / (kR0XP / 2);
+        dma16(pl ? rXl : rXh, xsrc(kb) + (unsigned)t0 * 64u,
+              lds_x + (unsigned)(pl * kR0XPL * 2 + (kb % (kR0XP / 2)) * 1024));
+      }
+    };
+    x_dma();
 
     // ---- k-loop: acc = [A0 | A1] [B0 ; B1] on the f16 split ----
     f32x16 acc[TM][CT];
@@ -233,7 +241,8 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         *reinterpret_cast<u16x8*>(Bs + p * kR0BPL + swz16(rem >> 1, rem & 1)) = st.rb[i];
       }
     };
-    auto compute = [&](int buf, bool one) {
+    auto compute = [&](int buf, auto one_c) {
+      constexpr bool one = decltype(one_c)::value;
       const unsigned short* As = smem + buf * kR0STG;
       const unsigned short* Bs = As + 2 * kR0APL;
       f16x8 bh[CT], bl[CT];
@@ -247,7 +256,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       for (int tm = 0; tm < TM; ++tm) {
         const int ao = swz16(32 * tm + lr, lh);
         const f16x8 ah = *reinterpret_cast<const f16x8*>(As + ao);
-        if (one) {
+        if constexpr (one) {
 #pragma unroll
           for (int tn = 0; tn < CT; ++tn)
             acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[tn], acc[tm][tn], 0, 0, 0);
@@ -258,49 +267,62 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         }
       }
     };
-    auto step = [&](int buf, int t) {
-      if (NSEG > 1 && t == nk) {
-        asm volatile("; segment switch" ::: "memory");   // a real branch (rowgemm3_kernel)
-        const float f = __builtin_ldexpf(1.0f, eP1 - eP0);
+    if (R0_ABL == 3) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < CT; ++j) acc[i][j] *= f;
-      }
-      compute(buf, t >= nk ? one1 : one0);
-    };
-    if (R0_PF == 1) {
-      Stage S;
-      gload(S, 0);
-      sstore(S, 0, false);
+        for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{} + 1.0f;
+    } else {
+      // two k-tiles of loads in flight, one loop over both segments (nk even: rbwd0_eligible K % 32 == 0)
+#if R0_PF == 4
+      // four k-tiles of loads in flight: stage S_(j % 4) holds k-tile j from its load, issued three steps
+      // ahead, until its LDS store (ntiles is a multiple of 4: rbwd0_eligible K % 32 == 0)
+      Stage S0, S1, S2, S3;
+      auto cl = [&](int j) { return j < ntiles ? j : ntiles - 1; };   // unconditional loads: exact vmcnt
+      gload(S0, 0);
+      gload(S1, cl(1));
+      gload(S2, cl(2));
+      gload(S3, cl(3));
+      sstore(S0, 0, false);
       lds_barrier();
-      for (int t = 0; t < ntiles; ++t) {
-        if (t + 1 < ntiles) gload(S, t + 1);
-        step(t & 1, t);
-        if (t + 1 < ntiles) sstore(S, (t + 1) & 1, t + 1 >= nk);
+      for (int t = 0; t < ntiles; t += 4) {
+        gload(S0, cl(t + 4));
+        compute(0, std::false_type{});
+        sstore(S1, 1, t + 1 >= nk);
+        lds_barrier();
+        gload(S1, cl(t + 5));
+        compute(1, std::false_type{});
+        sstore(S2, 0, t + 2 >= nk);
+        lds_barrier();
+        gload(S2, cl(t + 6));
+        compute(0, std::false_type{});
+        sstore(S3, 1, t + 3 >= nk);
+        lds_barrier();
+        gload(S3, cl(t + 7));
+        compute(1, std::false_type{});
+        if (t + 4 < ntiles) sstore(S0, 0, t + 4 >= nk);
         lds_barrier();
       }
-    } else {
+#else
       Stage S0, S1;
       gload(S0, 0);
       gload(S1, ntiles > 1 ? 1 : 0);
       sstore(S0, 0, false);
       lds_barrier();
-      int t = 0;
-      for (; t + 1 < ntiles; t += 2) {
+      for (int t = 0; t < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
-        step(0, t);
+        compute(0, std::false_type{});
         sstore(S1, 1, t + 1 >= nk);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
-        step(1, t + 1);
+        compute(1, std::false_type{});
         if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
         lds_barrier();
       }
-      if (t < ntiles) step(0, t);
+#endif
     }
     {
-      const float f = __builtin_ldexpf(1.0f, -(NSEG > 1 ? eP1 : eP0));
+      const float f = __builtin_ldexpf(1.0f, -eP);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -325,6 +347,11 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         for (int j = 0; j < EC; ++j) {
           const int r = EC * hf + j;
           const int so = (32 * tm + (r & 3) + 8 * (r >> 2)) * Npad * 4;
+          if constexpr (R0_ABL == 2) {
+            d[0][j] = 0.5f;
+            d[1][j] = d[2][j] = 0.25f;
+            continue;
+          }
           d[0][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rH, vo, so, 0));
           if constexpr (kE) {
             d[1][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, vo, so, 0));
@@ -370,7 +397,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
     float mt = 0.0f;
 #pragma unroll
     for (int u = 0; u < kR0NW; ++u) mt = fmaxf(mt, sMax[u]);
-    if (mt > 0.0f) {
+    if (R0_ABL != 1 && mt > 0.0f) {
       // RD_0's tile exponent; the accumulator follows the smallest one so far (no f16 overflow)
       const int et = f16_scale_exp(mt);
       if (et < Eacc) {
@@ -446,7 +473,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 }  // namespace
 
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K) {
-  return obs_pad <= 128 && x_ldp <= 128 && hid_pad <= 256 && hid_pad % 32 == 0 && K >= 4 && K % 4 == 0;
+  return obs_pad <= 128 && x_ldp <= 128 && hid_pad <= 256 && hid_pad % 32 == 0 && K >= 32 && K % 32 == 0;
 }
 
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
@@ -459,8 +486,7 @@ void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
   if ((int64_t)a.splits * a.rows_per_split < a.rows) throw std::runtime_error("rbwd0: splits do not cover the rows");
   if (a.nseg != 1 && a.nseg != 2) throw std::runtime_error("rbwd0: nseg must be 1 or 2");
   if ((a.nseg == 2) != (a.E != nullptr)) throw std::runtime_error("rbwd0: the E RH term goes with two segments");
-  RBwd0Args b = a;
-  b.low_seg = g_options.low_seg;
+  const RBwd0Args& b = a;
   if (a.nseg == 2) hipLaunchKernelGGL(rbwd0_kernel<2>, dim3(a.splits), dim3(kR0NT), 0, s, b);
   else hipLaunchKernelGGL(rbwd0_kernel<1>, dim3(a.splits), dim3(kR0NT), 0, s, b);
 }
