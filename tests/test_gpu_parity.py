@@ -822,7 +822,10 @@ def test_e16_planes_exact_and_truncated(gpu_available, obs, hidden, A, n):
     (37, [192, 200], 17, 2500),        # obs 37 (X planes 64 wide), hidden 192 (two idle waves), K = 200
     (128, [256], 18, 1500),            # one hidden layer: the policy gradient's backward only (FVP in the tail)
     (64, [256, 256, 256], 20, 900),    # depth 3
-], ids=["c4_dims", "odd", "one_hidden", "depth3"])
+    (128, [256, 160], 18, 1100),       # K = 160: 10 k-tiles per segment (the policy gradient's is not a multiple of 4)
+    (100, [256, 200], 7, 700),         # K = 200: a partial last k-tile, 13 per segment
+    (128, [256], 40, 800),             # one hidden layer, 40 actions (no tail): K = 40 for both backward paths
+], ids=["c4_dims", "odd", "one_hidden", "depth3", "k160", "k200", "one_hidden_a40"])
 def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
     """rbwd0.hip: layer 1's R-backward with layer 0's weight R-gradient in one launch (RD_0 never stored),
     and the same for the policy gradient's DS_0 (trpo_inksci.py:54,56-70), against the per-layer kernels

@@ -104,9 +104,12 @@ __device__ __forceinline__ void pl_dma4(__amdgpu_buffer_rsrc_t rsrc, unsigned vo
   }
 }
 
-template <int EPI>
+// NSEG: 1 (layer 0's X-only GEMMs: no second-segment loops or one-product variants to keep registers for)
+// or 2 (the runtime args.nseg)
+template <int EPI, int NSEG>
 __global__ void __launch_bounds__(kPlNW * 64, 2)
 rowgemm_pl_kernel(const RowGemmArgs args) {
+  constexpr bool kTwo = NSEG > 1;
   constexpr int WM = kPlWM, WN = kPlWN, TM = kPlTM, TN = kPlTN, BM = kPlBM, BN = kPlBN;
   constexpr int SA = kPlSA, SB = kPlSB;
   __shared__ __attribute__((aligned(16))) unsigned char sm[kPlLDS];
@@ -124,9 +127,9 @@ rowgemm_pl_kernel(const RowGemmArgs args) {
   const int eA0 = *args.seg[0].eAp;
   const int eP0 = __builtin_amdgcn_readfirstlane(eA0 + amax_exp(args.seg[0].amaxB));
   int eP1 = 0;
-  if (args.nseg > 1) eP1 = __builtin_amdgcn_readfirstlane(*args.seg[1].eAp + amax_exp(args.seg[1].amaxB));
+  if (kTwo && args.nseg > 1) eP1 = __builtin_amdgcn_readfirstlane(*args.seg[1].eAp + amax_exp(args.seg[1].amaxB));
   int one0 = 0, one1 = 0;
-  if (args.low_seg > 0 && args.nseg > 1) {
+  if (kTwo && args.low_seg > 0 && args.nseg > 1) {
     const int pen0 = (!args.seg[0].amaxA || !args.seg[0].amaxB) ? 4 : 0;
     const int pen1 = (!args.seg[1].amaxA || !args.seg[1].amaxB) ? 4 : 0;
     const int q0 = amax_exp(args.seg[0].amaxA) + amax_exp(args.seg[0].amaxB);
@@ -135,7 +138,7 @@ rowgemm_pl_kernel(const RowGemmArgs args) {
     one1 = __builtin_amdgcn_readfirstlane(q1 - q0 >= args.low_seg + pen0 ? 1 : 0);
   }
   const int ns0 = one0 ? (args.seg[0].K + 63) / 64 : (args.seg[0].K + 31) / 32;
-  const int ns1 = args.nseg > 1 ? (one1 ? (args.seg[1].K + 63) / 64 : (args.seg[1].K + 31) / 32) : 0;
+  const int ns1 = kTwo && args.nseg > 1 ? (one1 ? (args.seg[1].K + 63) / 64 : (args.seg[1].K + 31) / 32) : 0;
   const int nst = ns0 + ns1;
   const uint16_t *ah0 = args.seg[0].Ah, *al0 = args.seg[0].Al, *b0 = args.seg[0].Bb;
   const uint16_t *ah1 = args.seg[1].Ah, *al1 = args.seg[1].Al, *b1 = args.seg[1].Bb;
@@ -200,7 +203,7 @@ rowgemm_pl_kernel(const RowGemmArgs args) {
     if (PL_ABLATE != 2)                                                                                          \
       pl_compute<ONE>(sm + (t % SA) * kPlStage, sm + (SA + t % SB) * kPlStage, acc, wm, wn, lr, lh);             \
   }
-  if (one0) PL_LOOP(0, ns0, true)
+  if (kTwo && one0) PL_LOOP(0, ns0, true)
   else PL_LOOP(0, ns0, false)
   if (ns1 > 0) {
     scale_acc<TM, TN>(acc, eP1 - eP0);
@@ -230,7 +233,8 @@ void launch_row_pl(const RowGemmArgs& a, hipStream_t s) {
   RowGemmArgs b = a;
   b.low_seg = g_options.low_seg;
   const long nblk = (long)((a.M + kPlBM - 1) / kPlBM) * (a.Npad / kPlBN);
-  hipLaunchKernelGGL((rowgemm_pl_kernel<EPI>), dim3((unsigned)nblk), dim3(kPlNW * 64), 0, s, b);
+  if (a.nseg == 1) hipLaunchKernelGGL((rowgemm_pl_kernel<EPI, 1>), dim3((unsigned)nblk), dim3(kPlNW * 64), 0, s, b);
+  else hipLaunchKernelGGL((rowgemm_pl_kernel<EPI, 2>), dim3((unsigned)nblk), dim3(kPlNW * 64), 0, s, b);
 }
 
 }  // namespace

@@ -273,10 +273,10 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 #pragma unroll
         for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{} + 1.0f;
     } else {
-      // two k-tiles of loads in flight, one loop over both segments (nk even: rbwd0_eligible K % 32 == 0)
+      // two k-tiles of loads in flight, one loop over both segments
 #if R0_PF == 4
       // four k-tiles of loads in flight: stage S_(j % 4) holds k-tile j from its load, issued three steps
-      // ahead, until its LDS store (ntiles is a multiple of 4: rbwd0_eligible K % 32 == 0)
+      // ahead, until its LDS store
       Stage S0, S1, S2, S3;
       auto cl = [&](int j) { return j < ntiles ? j : ntiles - 1; };   // unconditional loads: exact vmcnt
       gload(S0, 0);
@@ -286,20 +286,21 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       sstore(S0, 0, false);
       lds_barrier();
       for (int t = 0; t < ntiles; t += 4) {
+        // steps past the last k-tile (ntiles % 4 != 0) only keep the load pattern (uniform branches)
         gload(S0, cl(t + 4));
         compute(0, std::false_type{});
-        sstore(S1, 1, t + 1 >= nk);
+        if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
         lds_barrier();
         gload(S1, cl(t + 5));
-        compute(1, std::false_type{});
-        sstore(S2, 0, t + 2 >= nk);
+        if (t + 1 < ntiles) compute(1, std::false_type{});
+        if (t + 2 < ntiles) sstore(S2, 0, t + 2 >= nk);
         lds_barrier();
         gload(S2, cl(t + 6));
-        compute(0, std::false_type{});
-        sstore(S3, 1, t + 3 >= nk);
+        if (t + 2 < ntiles) compute(0, std::false_type{});
+        if (t + 3 < ntiles) sstore(S3, 1, t + 3 >= nk);
         lds_barrier();
         gload(S3, cl(t + 7));
-        compute(1, std::false_type{});
+        if (t + 3 < ntiles) compute(1, std::false_type{});
         if (t + 4 < ntiles) sstore(S0, 0, t + 4 >= nk);
         lds_barrier();
       }
@@ -312,10 +313,10 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       for (int t = 0; t < ntiles; t += 2) {
         gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
         compute(0, std::false_type{});
-        sstore(S1, 1, t + 1 >= nk);
+        if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
         lds_barrier();
         gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
-        compute(1, std::false_type{});
+        if (t + 1 < ntiles) compute(1, std::false_type{});
         if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
         lds_barrier();
       }
@@ -473,7 +474,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 }  // namespace
 
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K) {
-  return obs_pad <= 128 && x_ldp <= 128 && hid_pad <= 256 && hid_pad % 32 == 0 && K >= 32 && K % 32 == 0;
+  return obs_pad <= 128 && x_ldp <= 128 && hid_pad <= 256 && hid_pad % 32 == 0 && K >= 4 && K % 4 == 0;
 }
 
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
