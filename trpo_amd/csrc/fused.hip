@@ -50,8 +50,11 @@ __device__ __forceinline__ int fswz(int r) { return ((r >> 1) & 1) | (((r >> 3) 
 __device__ __forceinline__ int fimg(int r, int f) { return r * kFI + ((((f >> 4) ^ fswz(r))) << 4) + (f & 15); }
 
 // NL = layers (2: one hidden layer, 3: two), FW = waves per workgroup, OBC = 64-wide chunks of obs
+#ifndef FUSED_LB
+#define FUSED_LB 2   // workgroups per CU the register budget is sized for (A/B builds: 1)
+#endif
 template <int NL, int FW, int OBC>
-__global__ void __launch_bounds__(FW * 64, 2) fvp_fused_kernel(const FusedArgs fa) {
+__global__ void __launch_bounds__(FW * 64, FUSED_LB) fvp_fused_kernel(const FusedArgs fa) {
   constexpr int OTM = 4;                      // 16-feature tiles of a hidden layer
   constexpr int NT = FW * 64;
   constexpr int CHU = 12 * 16 * OTM;          // 16-B units of the largest weight chunk
