@@ -40,6 +40,10 @@ struct trpo_engine {
   int device = 0;
   int num_cus = 256;               // compute units of `device` (hipDeviceAttributeMultiprocessorCount)
   hipStream_t stream = nullptr;
+  // second stream for the FVP's weight gradients, which run beside the R-backward (option dual); joined
+  // back into `stream` by events, so the pattern is capturable
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // policy shape
   int L = 0;                       // layers
   std::vector<int> w, wp;          // widths [obs, hidden..., A] and padded
@@ -301,6 +305,9 @@ struct trpo_engine {
     use();
     HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     w.push_back(obs);
     for (int i = 0; i < nh; ++i) w.push_back(hidden[i]);
     w.push_back(A);
@@ -585,6 +592,10 @@ struct trpo_engine {
     free_har_slots();
     if (hsc) (void)hipHostFree(hsc);
     if (comm) (void)ncclCommDestroy(comm);
+    if (side) (void)hipStreamSynchronize(side);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -1147,58 +1158,78 @@ struct trpo_engine {
     const bool tail_fused = fused_head || head_bwd || tail;
     // layer 1's R-backward fused with layer 0's weight gradient when layer 1 is not inside the tail
     const bool r0f = use_rbwd0() && (tail_fused ? L - 2 : L - 1) >= 1;
-    // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
-    for (int l = tail_fused ? L - 2 : L - 1; l >= 1; --l) {
-      if (l == 1 && r0f) {
-        RBwd0Args a = rbwd0_args(skip);
+    auto r_backward = [&]() {
+      // R-backward: RDH_l = RD_l W_l^T + D_l V_l^T ; RD_{l-1} = RDH (1-H_l^2) + E_{l-1} RH_l
+      for (int l = tail_fused ? L - 2 : L - 1; l >= 1; --l) {
+        if (l == 1 && r0f) {
+          RBwd0Args a = rbwd0_args(skip);
+          a.nseg = 2;
+          a.A0 = RD[1];
+          a.A1 = D[1];
+          a.am_a0 = am_rd(1);
+          a.am_a1 = am_d(1);
+          a.E = E[0];
+          a.RH = RH[1];
+          Scope sp(this, "fvp_rbwdwg_l1");
+          launch_rbwd0(a, stream);
+          check_launch();
+          continue;
+        }
+        RowGemmArgs a = row_args(w[l], wp[l]);
         a.nseg = 2;
-        a.A0 = RD[1];
-        a.A1 = D[1];
-        a.am_a0 = am_rd(1);
-        a.am_a1 = am_d(1);
-        a.E = E[0];
-        a.RH = RH[1];
-        Scope sp(this, "fvp_rbwdwg_l1");
-        launch_rbwd0(a, stream);
+        a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
+        a.seg[1] = GemmSeg{D[l], WB[l] + (size_t)wp[l + 1] * wp[l], wp[l + 1], wp[l], wp[l + 1]};
+        seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
+        seg3(a.seg[1], WB3[l], plane3_b(l), 1, wp[l + 1]);
+        a.seg[0].amaxA = am_rd(l);
+        a.seg[0].amaxB = am_w(l);
+        a.seg[1].amaxA = am_d(l);
+        a.seg[1].amaxB = am_v(l);
+        a.skip = skip;
+        a.epi = prep_e16 ? RowEpi::kRBwd16 : RowEpi::kRBwd;
+        a.ea.H = H[l];
+        a.ea.E = E[l - 1];
+        a.ea.e16_lo = e16_lo(l - 1);
+        a.ea.amaxE = am_e(l - 1);
+        a.ea.amaxRH = am_rh(l);
+        a.ea.RH = RH[l];
+        a.ea.out0 = RD[l - 1];
+        a.ea.amax0 = am_rd(l - 1);
+        a.ea.ldo = wp[l];
+        char tag[32];
+        std::snprintf(tag, sizeof tag, "fvp_rbwd_l%d", l);
+        Scope sp(this, tag);
+        launch_rowgemm(a, stream);
         check_launch();
-        continue;
       }
-      RowGemmArgs a = row_args(w[l], wp[l]);
-      a.nseg = 2;
-      a.seg[0] = GemmSeg{RD[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
-      a.seg[1] = GemmSeg{D[l], WB[l] + (size_t)wp[l + 1] * wp[l], wp[l + 1], wp[l], wp[l + 1]};
-      seg3(a.seg[0], WB3[l], plane3_b(l), 0, wp[l + 1]);
-      seg3(a.seg[1], WB3[l], plane3_b(l), 1, wp[l + 1]);
-      a.seg[0].amaxA = am_rd(l);
-      a.seg[0].amaxB = am_w(l);
-      a.seg[1].amaxA = am_d(l);
-      a.seg[1].amaxB = am_v(l);
-      a.skip = skip;
-      a.epi = prep_e16 ? RowEpi::kRBwd16 : RowEpi::kRBwd;
-      a.ea.H = H[l];
-      a.ea.E = E[l - 1];
-      a.ea.e16_lo = e16_lo(l - 1);
-      a.ea.amaxE = am_e(l - 1);
-      a.ea.amaxRH = am_rh(l);
-      a.ea.RH = RH[l];
-      a.ea.out0 = RD[l - 1];
-      a.ea.amax0 = am_rd(l - 1);
-      a.ea.ldo = wp[l];
-      char tag[32];
-      std::snprintf(tag, sizeof tag, "fvp_rbwd_l%d", l);
-      Scope sp(this, tag);
-      launch_rowgemm(a, stream);
-      check_launch();
-    }
-    // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
-    for (int l = r0f ? 1 : 0; l < (tail_fused ? L - 1 : L); ++l) {
-      char tag[32];
-      std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
-      if (l == 0)
-        wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1], am_x(), am_rd(0)}, WSeg{}, 0, skip, tag);
-      else
-        wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)},
-                    WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
+    };
+    auto weight_grads = [&]() {
+      // weight gradients: (Hv)_W_l = RH_l^T D_l + H_l^T RD_l ; (Hv)_b_l = colsum RD_l
+      for (int l = r0f ? 1 : 0; l < (tail_fused ? L - 1 : L); ++l) {
+        char tag[32];
+        std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
+        if (l == 0)
+          wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1], am_x(), am_rd(0)}, WSeg{}, 0, skip, tag);
+        else
+          wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)},
+                      WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
+      }
+    };
+    // With two hidden layers under the tail and the fused layer-1 R-backward, the one weight-gradient GEMM left
+    // (layer 1: RH1, D1, H1 and the tail's RD1) does not depend on the R-backward: with option dual it runs on
+    // the side stream beside it (fork / join events; captured like the rest of the prefix)
+    if (g_options.dual != 0 && side && r0f && tail_fused && L == 3) {
+      HIPCHECK(hipEventRecord(ev_fork, stream));
+      HIPCHECK(hipStreamWaitEvent(side, ev_fork, 0));
+      std::swap(stream, side);
+      weight_grads();
+      std::swap(stream, side);
+      r_backward();
+      HIPCHECK(hipEventRecord(ev_join, side));
+      HIPCHECK(hipStreamWaitEvent(stream, ev_join, 0));
+    } else {
+      r_backward();
+      weight_grads();
     }
     reduce_grad(out, skip);
   }
@@ -2367,6 +2398,7 @@ static int* option_slot(const std::string& k) {
   if (k == "planes") return &g_options.planes;
   if (k == "e16") return &g_options.e16;
   if (k == "rbwd0") return &g_options.rbwd0;
+  if (k == "dual") return &g_options.dual;
   throw ArgError("unknown option " + k);
 }
 

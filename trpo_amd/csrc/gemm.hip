@@ -39,7 +39,8 @@ Options g_options = {env_int("TRPO_ROWCFG", 0), env_int("TRPO_WGCFG", 0), env_in
                      env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1), env_int("TRPO_SPLIT_F16", 1),
                      env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1), env_int("TRPO_TAIL", 1),
                      env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14), env_int("TRPO_PLANES", 1),
-                     env_int("TRPO_E16", 0), env_int("TRPO_RBWD0", 1)};
+                     env_int("TRPO_E16", 0), env_int("TRPO_RBWD0", 1),
+                     env_int("TRPO_DUAL", 0)};
 
 namespace {
 

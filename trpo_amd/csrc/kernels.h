@@ -34,6 +34,7 @@ struct Options {
                    // high/low planes (RowEpi::kRBwd16): 0 off (f32), 1 on
   int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
+  int dual;        // engine: the FVP's weight-gradient GEMMs on a second stream beside the R-backward: 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
