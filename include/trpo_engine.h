@@ -206,7 +206,13 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * the register-staged split; default 1), "e16" (1 = the tanh'' terms E_l that the per-layer R-backward
  * row GEMMs read are stored as the 16-bit high and low halves of each f32 word; the R-backward reads
  * both halves (the f32 value, bit for bit) or, when the E RH term's running-max product scale lies
- * low_seg + 3 binades below the main term's, the high halves alone; default 0: at C4 the test does not fire and the two 16-bit loads cost more than one f32 load).
+ * low_seg + 3 binades below the main term's, the high halves alone; default 0: at C4 the test does not fire and the two 16-bit loads cost more than one f32 load),
+ * "rbwd0" (1 = layer 1's R-backward and layer 0's weight gradient run as one launch of rbwd0.hip:
+ * RD_0 stays in registers and X^T RD_0 is reduced from the engine's X planes; eligible on the f16
+ * split with planes on, obs <= 128, hidden widths <= 256 and multiples of 32; also serves the policy
+ * gradient's layer-1 backward; default 1), "dual" (1 = the FVP's layer-1 weight gradient runs on a
+ * second stream beside the fused R-backward, joined by events and capturable in the update graph;
+ * needs rbwd0, the fused tail and two hidden layers; default 0: slower at C4).
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

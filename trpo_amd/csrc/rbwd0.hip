@@ -37,17 +37,26 @@ namespace {
 #ifndef R0_EC
 #define R0_EC 4      // epilogue chunk: accumulator registers per load batch
 #endif
-#ifndef R0_PF
-#define R0_PF 4      // k-tiles of A / B loads in flight (register stages): 2 or 4
-#endif
 #ifndef R0_NW
 #define R0_NW 8      // waves per workgroup
+#endif
+#ifndef R0_BK
+#define R0_BK 32     // k per staged k-tile: 16 (32-B LDS rows) or 32 (64-B rows; the X image then reuses the
+                     // staging buffers after the k-loop). C4 A/B (profiles/r3j): 12.04 ms at 32 / PF 2 against
+                     // 12.83 at 16 / PF 4
+#endif
+#ifndef R0_PF
+#if R0_BK == 32
+#define R0_PF 2      // k-tiles of A / B loads in flight (register stages): 2 or 4
+#else
+#define R0_PF 4
+#endif
 #endif
 constexpr int kR0Rows = R0_ROWS;              // rows per tile
 constexpr int kR0NW = R0_NW;                  // waves
 constexpr int kR0CT = 8 / kR0NW;              // 32-column tiles per wave: wave w owns RD_0 columns [32 CT w, ..)
 constexpr int kR0NT = kR0NW * 64;             // threads
-constexpr int kR0BK = 16;
+constexpr int kR0BK = R0_BK;
 constexpr int kR0TM = kR0Rows / 32;           // accumulator row tiles per wave (all rows of the tile)
 constexpr int kR0XT = 4;                      // 32-column tiles of X (obs <= 128)
 constexpr int kR0APL = kR0Rows * kR0BK;       // u16 per A plane per stage
@@ -58,8 +67,18 @@ constexpr int kR0AI = kR0APL / 4 / kR0NT;     // f32x4 A staging items per threa
 constexpr int kR0BI = 2 * kR0BPL / 8 / kR0NT; // u16x8 B staging items per thread
 constexpr int kR0XP = 2 * kR0XPL * 2 / 1024;  // 1-KB X DMA pieces per tile (both planes)
 constexpr int kR0XD = kR0XP / kR0NW;          // ... per wave
-constexpr int kR0LDSU = 2 * kR0STG + 2 * kR0XPL;   // u16: two staging buffers + the X image
+constexpr bool kR0XAlias = (2 * kR0STG + 2 * kR0XPL) * 2 + 64 > 160 * 1024;   // X image in the staging bytes
+constexpr int kR0LDSU = kR0XAlias ? (2 * kR0STG > 2 * kR0XPL ? 2 * kR0STG : 2 * kR0XPL) : 2 * kR0STG + 2 * kR0XPL;
 static_assert(kR0LDSU * 2 <= 160 * 1024, "rbwd0 LDS");
+static_assert(kR0BK == 16 || kR0BK == 32, "rbwd0 k-tile");
+
+// u16 offset of the 16-B chunk c (8 k) of row r in a staged [row][kR0BK] f16 image: 32-B rows flip their two
+// chunks on row bit 2 ^ bit 3 (swz16), 64-B rows XOR theirs with row bits 2-3 (plane.hip's pl_swz); both keep
+// the ds_read_b128 fragment reads of a 16-lane group on 16 distinct bank slots
+__device__ __forceinline__ int swzk(int r, int c) {
+  if constexpr (kR0BK == 16) return swz16(r, c);
+  else return r * 32 + ((c ^ ((r >> 2) & 3)) << 3);
+}
 static_assert(kR0AI >= 1 && kR0APL % (4 * kR0NT) == 0 && kR0XP % kR0NW == 0, "rbwd0 tile shape");
 
 // byte offset of the 16-B chunk `ch` (8 obs) of `row` in an X plane image: 8-row x 32-column subtiles of
@@ -142,7 +161,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   const unsigned xbytes = (unsigned)A.x_ldp * (unsigned)A.x_mpad * 2u;
   const __amdgpu_buffer_rsrc_t rXh = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xh, 0, xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rXl = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xl, 0, xbytes, 0x00020000);
-  unsigned short* const sX = smem + 2 * kR0STG;
+  unsigned short* const sX = smem + (kR0XAlias ? 0 : 2 * kR0STG);
   const unsigned lds_x = (unsigned)(uintptr_t)sX;
 
   // lane-dependent values are recomputed per tile from an opaque copy of the thread id: hoisted out of
@@ -183,7 +202,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
               lds_x + (unsigned)(pl * kR0XPL * 2 + (kb % (kR0XP / 2)) * 1024));
       }
     };
-    x_dma();
+    if (!kR0XAlias) x_dma();
 
     // ---- k-loop: acc = [A0 | A1] [B0 ; B1] on the f16 split ----
     f32x16 acc[TM][CT];
@@ -205,14 +224,16 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
                                                                           0x00020000);
 #pragma unroll
       for (int i = 0; i < kR0AI; ++i) {
-        const int f = tid + i * kR0NT, r = f >> 2, kq = f & 3;
+        const int f = tid + i * kR0NT, r = f / (kR0BK / 4), kq = f % (kR0BK / 4);
         const int vo = (k0 + kR0BK > K && k0 + 4 * kq >= K) ? kOob : (r * lda + 4 * kq) * 4;
         st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, k0 * 4, 0));
       }
 #pragma unroll
       for (int i = 0; i < kR0BI; ++i) {
-        const int f = tid + i * kR0NT, p = f >> 9, rem = f & 511, n = rem >> 1, kh = rem & 1;
-        const int vo = n < Npad ? (int)((p * A.plane + (int64_t)n * A.ldk + 8 * kh) * 2) : kOob;
+        constexpr int CB = kR0BK / 8;   // 16-B chunks per column and k-tile
+        const int f = tid + i * kR0NT, p = f / (256 * CB), rem = f % (256 * CB), n = rem / CB, kh = rem % CB;
+        // columns past Npad and k past the planes' ldk (the next column's row) read 0
+        const int vo = (n < Npad && k0 + 8 * kh < A.ldk) ? (int)((p * A.plane + (int64_t)n * A.ldk + 8 * kh) * 2) : kOob;
         st.rb[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rB, vo, k0 * 2, 0));
       }
     };
@@ -222,7 +243,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       const float sa = s1 ? sA1 : sA0;
 #pragma unroll
       for (int i = 0; i < kR0AI; ++i) {
-        const int f = tid + i * kR0NT, r = f >> 2, kq = f & 3;
+        const int f = tid + i * kR0NT, r = f / (kR0BK / 4), kq = f % (kR0BK / 4);
         u16x4 h, l;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -231,39 +252,43 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
           h[j] = hh;
           l[j] = ll;
         }
-        unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
+        unsigned short* dst = As + swzk(r, kq >> 1) + 4 * (kq & 1);
         *reinterpret_cast<u16x4*>(dst) = h;
         *reinterpret_cast<u16x4*>(dst + kR0APL) = l;
       }
 #pragma unroll
       for (int i = 0; i < kR0BI; ++i) {
-        const int f = tid + i * kR0NT, p = f >> 9, rem = f & 511;
-        *reinterpret_cast<u16x8*>(Bs + p * kR0BPL + swz16(rem >> 1, rem & 1)) = st.rb[i];
+        constexpr int CB = kR0BK / 8;
+        const int f = tid + i * kR0NT, p = f / (256 * CB), rem = f % (256 * CB);
+        *reinterpret_cast<u16x8*>(Bs + p * kR0BPL + swzk(rem / CB, rem % CB)) = st.rb[i];
       }
     };
     auto compute = [&](int buf, auto one_c) {
       constexpr bool one = decltype(one_c)::value;
       const unsigned short* As = smem + buf * kR0STG;
       const unsigned short* Bs = As + 2 * kR0APL;
-      f16x8 bh[CT], bl[CT];
 #pragma unroll
-      for (int tn = 0; tn < CT; ++tn) {
-        const int bo = swz16(col0 + 32 * tn + lr, lh);
-        bh[tn] = *reinterpret_cast<const f16x8*>(Bs + bo);
-        bl[tn] = *reinterpret_cast<const f16x8*>(Bs + kR0BPL + bo);
-      }
+      for (int ks = 0; ks < kR0BK / 16; ++ks) {   // 16-k MFMA steps of the staged k-tile
+        f16x8 bh[CT], bl[CT];
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int ao = swz16(32 * tm + lr, lh);
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(As + ao);
-        if constexpr (one) {
+        for (int tn = 0; tn < CT; ++tn) {
+          const int bo = swzk(col0 + 32 * tn + lr, 2 * ks + lh);
+          bh[tn] = *reinterpret_cast<const f16x8*>(Bs + bo);
+          bl[tn] = *reinterpret_cast<const f16x8*>(Bs + kR0BPL + bo);
+        }
 #pragma unroll
-          for (int tn = 0; tn < CT; ++tn)
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[tn], acc[tm][tn], 0, 0, 0);
-        } else {
-          const f16x8 al = *reinterpret_cast<const f16x8*>(As + kR0APL + ao);
+        for (int tm = 0; tm < TM; ++tm) {
+          const int ao = swzk(32 * tm + lr, 2 * ks + lh);
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(As + ao);
+          if constexpr (one) {
 #pragma unroll
-          for (int tn = 0; tn < CT; ++tn) acc[tm][tn] = mfma3h(ah, al, bh[tn], bl[tn], acc[tm][tn]);
+            for (int tn = 0; tn < CT; ++tn)
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[tn], acc[tm][tn], 0, 0, 0);
+          } else {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(As + kR0APL + ao);
+#pragma unroll
+            for (int tn = 0; tn < CT; ++tn) acc[tm][tn] = mfma3h(ah, al, bh[tn], bl[tn], acc[tm][tn]);
+          }
         }
       }
     };
@@ -321,6 +346,11 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         lds_barrier();
       }
 #endif
+    }
+    if (kR0XAlias) {
+      // the X image takes the staging buffers' bytes: every wave is past its last fragment read first
+      __syncthreads();
+      x_dma();
     }
     {
       const float f = __builtin_ldexpf(1.0f, -eP);
