@@ -519,6 +519,7 @@ struct RBwd0Args {
   float* slab;
   int64_t slab_stride, off_w, off_b;
   const int* skip;
+  int low_seg = 0;          // f16: segment 1 on one product when it sits >= low_seg binades under (set at launch)
 };
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s);

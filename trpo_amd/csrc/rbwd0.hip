@@ -152,6 +152,14 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   const int eA1 = NSEG > 1 ? amax_exp(A.am_a1) : 0, eB1 = NSEG > 1 ? amax_exp(A.am_b1) : 0;
   const int eP = NSEG > 1 ? min(eA0 + eB0, eA1 + eB1) : eA0 + eB0;
   const float sA0 = __builtin_ldexpf(1.0f, eP - eB0), sA1 = __builtin_ldexpf(1.0f, eP - eB1);
+  // segment 1 (D_1 V_1^T) >= low_seg binades under segment 0 (the per-layer kernels' test, rowgemm3_kernel):
+  // its tiles run hi x hi alone. At the shared scale its lo planes sit >= low_seg binades under their own
+  // optimum, so the two dropped products are 2^-11 of the segment, 2^-(11 + low_seg) of the output
+  int one1 = 0;
+  if (NSEG > 1 && A.low_seg > 0) {
+    const int pen0 = (!A.am_a0 || !A.am_b0) ? 4 : 0;
+    one1 = __builtin_amdgcn_readfirstlane((eA1 + eB1) - (eA0 + eB0) >= A.low_seg + pen0 ? 1 : 0);
+  }
   const int eX = __builtin_amdgcn_readfirstlane(*A.eX);
 
   const int nk = (K + kR0BK - 1) / kR0BK;     // k-tiles per segment
@@ -274,7 +282,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         for (int tn = 0; tn < CT; ++tn) {
           const int bo = swzk(col0 + 32 * tn + lr, 2 * ks + lh);
           bh[tn] = *reinterpret_cast<const f16x8*>(Bs + bo);
-          bl[tn] = *reinterpret_cast<const f16x8*>(Bs + kR0BPL + bo);
+          if constexpr (!one) bl[tn] = *reinterpret_cast<const f16x8*>(Bs + kR0BPL + bo);
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
@@ -298,7 +306,9 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 #pragma unroll
         for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{} + 1.0f;
     } else {
-      // two k-tiles of loads in flight, one loop over both segments
+      // segment 1's tiles on one product run as a second loop over [t1, ntiles) (t1 = nk, a multiple of the
+      // unroll; the loops' bodies differ only in the compute step -- a branch inside one loop spills)
+      const int t1 = (one1 && nk % R0_PF == 0) ? nk : ntiles;
 #if R0_PF == 4
       // four k-tiles of loads in flight: stage S_(j % 4) holds k-tile j from its load, issued three steps
       // ahead, until its LDS store
@@ -310,42 +320,50 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       gload(S3, cl(3));
       sstore(S0, 0, false);
       lds_barrier();
-      for (int t = 0; t < ntiles; t += 4) {
-        // steps past the last k-tile (ntiles % 4 != 0) only keep the load pattern (uniform branches)
-        gload(S0, cl(t + 4));
-        compute(0, std::false_type{});
-        if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
-        lds_barrier();
-        gload(S1, cl(t + 5));
-        if (t + 1 < ntiles) compute(1, std::false_type{});
-        if (t + 2 < ntiles) sstore(S2, 0, t + 2 >= nk);
-        lds_barrier();
-        gload(S2, cl(t + 6));
-        if (t + 2 < ntiles) compute(0, std::false_type{});
-        if (t + 3 < ntiles) sstore(S3, 1, t + 3 >= nk);
-        lds_barrier();
-        gload(S3, cl(t + 7));
-        if (t + 3 < ntiles) compute(1, std::false_type{});
-        if (t + 4 < ntiles) sstore(S0, 0, t + 4 >= nk);
-        lds_barrier();
-      }
+      auto kloop = [&](int tb, int te, auto one_c) {
+        for (int t = tb; t < te; t += 4) {
+          // steps past the last k-tile (ntiles % 4 != 0) only keep the load pattern (uniform branches)
+          gload(S0, cl(t + 4));
+          compute(0, one_c);
+          if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
+          lds_barrier();
+          gload(S1, cl(t + 5));
+          if (t + 1 < ntiles) compute(1, one_c);
+          if (t + 2 < ntiles) sstore(S2, 0, t + 2 >= nk);
+          lds_barrier();
+          gload(S2, cl(t + 6));
+          if (t + 2 < ntiles) compute(0, one_c);
+          if (t + 3 < ntiles) sstore(S3, 1, t + 3 >= nk);
+          lds_barrier();
+          gload(S3, cl(t + 7));
+          if (t + 3 < ntiles) compute(1, one_c);
+          if (t + 4 < ntiles) sstore(S0, 0, t + 4 >= nk);
+          lds_barrier();
+        }
+      };
 #else
+      // two k-tiles of loads in flight
       Stage S0, S1;
       gload(S0, 0);
       gload(S1, ntiles > 1 ? 1 : 0);
       sstore(S0, 0, false);
       lds_barrier();
-      for (int t = 0; t < ntiles; t += 2) {
-        gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
-        compute(0, std::false_type{});
-        if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
-        lds_barrier();
-        gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
-        if (t + 1 < ntiles) compute(1, std::false_type{});
-        if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
-        lds_barrier();
-      }
+      auto kloop = [&](int tb, int te, auto one_c) {
+        for (int t = tb; t < te; t += 2) {
+          gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
+          compute(0, one_c);
+          if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
+          lds_barrier();
+          gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
+          if (t + 1 < ntiles) compute(1, one_c);
+          if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
+          lds_barrier();
+        }
+      };
 #endif
+      kloop(0, t1, std::false_type{});
+      __builtin_amdgcn_sched_barrier(0);
+      kloop(t1, ntiles, std::true_type{});
     }
     if (kR0XAlias) {
       // the X image takes the staging buffers' bytes: every wave is past its last fragment read first
@@ -517,7 +535,8 @@ void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
   if ((int64_t)a.splits * a.rows_per_split < a.rows) throw std::runtime_error("rbwd0: splits do not cover the rows");
   if (a.nseg != 1 && a.nseg != 2) throw std::runtime_error("rbwd0: nseg must be 1 or 2");
   if ((a.nseg == 2) != (a.E != nullptr)) throw std::runtime_error("rbwd0: the E RH term goes with two segments");
-  const RBwd0Args& b = a;
+  RBwd0Args b = a;
+  b.low_seg = g_options.low_seg;
   if (a.nseg == 2) hipLaunchKernelGGL(rbwd0_kernel<2>, dim3(a.splits), dim3(kR0NT), 0, s, b);
   else hipLaunchKernelGGL(rbwd0_kernel<1>, dim3(a.splits), dim3(kR0NT), 0, s, b);
 }
