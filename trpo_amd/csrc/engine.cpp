@@ -114,7 +114,12 @@ struct trpo_engine {
   // running max whenever X changes (layout stride x_mpad = round256(n)), and blocked copies of layer 0's
   // W / V weight planes, re-blocked from WF3 / WFt3 before each use
   uint16_t *Xh = nullptr, *Xl = nullptr, *W0b = nullptr, *V0b = nullptr;
-  int* pl_e = nullptr;   // scale exponents published by the plane producers: [0] = X
+  int* pl_e = nullptr;   // scale exponents published by the plane producers: [0] = X, [1] = D_1
+  // D_1's f16 hi plane (k-blocked like Xh, stride d1_mpad = round256(n)), written by prepare() for the fused
+  // R-backward's one-product D_1 V_1^T segment (rbwd0.hip)
+  uint16_t* D1h = nullptr;
+  int d1_mpad = 0, d1_ldp = 0;
+  bool d1_plane = false;   // D1h holds the current D_1
   int x_mpad = 0, x_ldp = 0;
   bool x_planes = false;   // Xh/Xl hold the current X
   bool planes_geom_l0() const {   // layer 0's row GEMMs fit the plane kernel
@@ -401,6 +406,10 @@ struct trpo_engine {
       W0b = dalloc<uint16_t>(2 * plane3_f(0));
       V0b = dalloc<uint16_t>(2 * plane3_f(0));
       pl_e = dalloc<int>(8);
+    }
+    if (f16 && L >= 2 && rbwd0_geom()) {
+      d1_ldp = (wp[2] + 31) / 32 * 32;
+      D1h = dalloc<uint16_t>((size_t)((cap + 255) / 256 * 256) * d1_ldp);
     }
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
@@ -892,6 +901,15 @@ struct trpo_engine {
       launch_rowgemm(a, stream);
       check_launch();
     }
+    // D_1's hi plane for the fused R-backward (per update; the FVPs' D_1 V_1^T segment reads half the bytes)
+    d1_plane = false;
+    if (D1h && use_rbwd0() && n > 0) {
+      d1_mpad = (int)((n + 255) / 256 * 256);
+      Scope sp(this, "split_d1");
+      launch_split_planes(D[1], (int)n, d1_mpad, wp[2], wp[2], D1h, nullptr, d1_ldp, am_d(1), pl_e + 1, stream);
+      check_launch();
+      d1_plane = true;
+    }
     reduce_losses(0, nullptr);
     prepared = true;
   }
@@ -1166,6 +1184,11 @@ struct trpo_engine {
           a.nseg = 2;
           a.A0 = RD[1];
           a.A1 = D[1];
+          if (d1_plane) {
+            a.A1h = D1h;
+            a.a1_mpad = d1_mpad;
+            a.eA1p = pl_e + 1;
+          }
           a.am_a0 = am_rd(1);
           a.am_a1 = am_d(1);
           a.E = E[0];

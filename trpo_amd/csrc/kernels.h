@@ -503,6 +503,9 @@ struct RBwd0Args {
   int nseg;                 // 2: [RD_1 | D_1] ; 1: DS_1 alone
   const float* A0;          // [rows][lda] RD_1 (or DS_1)
   const float* A1;          // [rows][lda] D_1
+  const uint16_t* A1h;      // D_1's k-blocked f16 hi plane (GemmSeg::Ah layout, scale 2^(*eA1p)); NULL: none
+  int a1_mpad;
+  const int* eA1p;
   const uint16_t* B0;       // f16 hi/lo planes of W_1^T: [2][Npad][ldk] (plane stride `plane`)
   const uint16_t* B1;       // ... of V_1^T
   int ldk;

@@ -268,25 +268,37 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
   const int e = amax_exp(amax);   // whole wave, before any exit
   if (blockIdx.x == 0 && threadIdx.x == 0 && e_out) *e_out = e;
   const float s = __builtin_ldexpf(1.0f, e);
-  // consecutive threads: consecutive 8-k chunks of one 32-k block of consecutive rows (coalesced stores)
-  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // consecutive threads: consecutive 8-k chunks of one 32-k block of consecutive rows (coalesced stores);
+  // a grid-stride loop over the chunks (one running-max read per thread, not per 8 values)
   const int64_t nchunk = (int64_t)Mpad * (ldp / 8);
-  if (f >= nchunk) return;
-  const int64_t kb = f / ((int64_t)Mpad * 4);
-  const int64_t rem = f % ((int64_t)Mpad * 4);
-  const int r = (int)(rem / 4), c = (int)(rem % 4);
-  f16x8 h, l;
+  const bool vec = (lda & 3) == 0;
+  for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < nchunk; f += (int64_t)gridDim.x * 256) {
+    const int64_t kb = f / ((int64_t)Mpad * 4);
+    const int64_t rem = f % ((int64_t)Mpad * 4);
+    const int r = (int)(rem / 4), c = (int)(rem % 4);
+    const int k0 = (int)kb * 32 + c * 8;
+    float x[8];
+    if (vec && r < M && k0 + 8 <= K) {
+      const float4 a = *reinterpret_cast<const float4*>(A + (int64_t)r * lda + k0);
+      const float4 b = *reinterpret_cast<const float4*>(A + (int64_t)r * lda + k0 + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    } else {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = (int)kb * 32 + c * 8 + j;
-    const float x = (r < M && k < K) ? A[(int64_t)r * lda + k] * s : 0.0f;
-    const _Float16 hh = (_Float16)x;
-    h[j] = hh;
-    l[j] = (_Float16)(x - (float)hh);
+      for (int j = 0; j < 8; ++j) x[j] = (r < M && k0 + j < K) ? A[(int64_t)r * lda + k0 + j] : 0.0f;
+    }
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = x[j] * s;
+      const _Float16 hh = (_Float16)v;
+      h[j] = hh;
+      l[j] = (_Float16)(v - (float)hh);
+    }
+    const int64_t o = (kb * Mpad + r) * 32 + c * 8;
+    *reinterpret_cast<f16x8*>(hi + o) = h;
+    if (lo) *reinterpret_cast<f16x8*>(lo + o) = l;
   }
-  const int64_t o = (kb * Mpad + r) * 32 + c * 8;
-  *reinterpret_cast<f16x8*>(hi + o) = h;
-  if (lo) *reinterpret_cast<f16x8*>(lo + o) = l;
 }
 
 // [P][R][ld] planes (k contiguous, ld a multiple of 32) -> k-blocked [P][ld / 32][R][32]
@@ -308,7 +320,8 @@ void launch_split_planes(const float* A, int M, int Mpad, int K, int lda, uint16
                          const unsigned* amax, int* e_out, hipStream_t s) {
   if (ldp % 32 || ldp < K || Mpad < M) throw std::runtime_error("split_planes: bad ldp / Mpad");
   const int64_t n = (int64_t)Mpad * (ldp / 8);
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, M, Mpad, K, lda, hi,
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, s, A, M, Mpad, K, lda, hi,
                      lo, ldp, amax, e_out);
 }
 

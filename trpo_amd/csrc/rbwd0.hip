@@ -153,8 +153,8 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   const int eP = NSEG > 1 ? min(eA0 + eB0, eA1 + eB1) : eA0 + eB0;
   const float sA0 = __builtin_ldexpf(1.0f, eP - eB0), sA1 = __builtin_ldexpf(1.0f, eP - eB1);
   // segment 1 (D_1 V_1^T) >= low_seg binades under segment 0 (the per-layer kernels' test, rowgemm3_kernel):
-  // its tiles run hi x hi alone. At the shared scale its lo planes sit >= low_seg binades under their own
-  // optimum, so the two dropped products are 2^-11 of the segment, 2^-(11 + low_seg) of the output
+  // its tiles run hi x hi alone on D_1's f16 hi plane (below), the dropped products 2^-11 of the segment,
+  // 2^-(11 + low_seg) of the output
   int one1 = 0;
   if (NSEG > 1 && A.low_seg > 0) {
     const int pen0 = (!A.am_a0 || !A.am_b0) ? 4 : 0;
@@ -164,6 +164,13 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 
   const int nk = (K + kR0BK - 1) / kR0BK;     // k-tiles per segment
   const int ntiles = NSEG * nk;
+  // sw: segment 1 on one product from the engine's per-update hi plane of D_1 (k-blocked, 64-B rows: one
+  // 16-B load per thread and k-tile, half the bytes of f32 D_1). Its tiles run FIRST, at the plane's own
+  // product scale 2^(eA1p + eB1); the accumulator then steps down to 2^eP (a power of two: exact) for
+  // segment 0. Without the plane (or with a k-tile count the unrolled loop cannot split) both run 3 products.
+  const int sw = (kR0BK == 32 && NSEG > 1 && A.A1h && one1 && nk % R0_PF == 0) ? 1 : 0;
+  const int eA1p = sw ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;
+  const float sDown = __builtin_ldexpf(1.0f, sw ? eP - (eA1p + eB1) : 0);
   const int bbytes = (int)(2 * A.plane * 2);
 
   const unsigned xbytes = (unsigned)A.x_ldp * (unsigned)A.x_mpad * 2u;
@@ -222,22 +229,33 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       f32x4 ra[kR0AI];
       u16x8 rb[kR0BI];
     };
+    // tile t: segment 1 is tiles [0, nk) under sw, [nk, 2 nk) otherwise; pt = a D_1 hi-plane tile
     auto gload = [&](Stage& st, int t) {
-      const bool s1 = t >= nk;
-      const float* Ap = s1 ? A.A1 : A.A0;
-      const int k0 = (s1 ? t - nk : t) * kR0BK;
-      const __amdgpu_buffer_rsrc_t rA =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(Ap + (size_t)t0 * lda), 0, Mt * lda * 4, 0x00020000);
+      const bool pt = sw && t < nk;
+      const bool s1 = sw ? t < nk : t >= nk;
+      const int kt = t >= nk ? t - nk : t;
+      const int k0 = kt * kR0BK;
+      if (pt) {
+        // rows past the tile's Mt read 0 (the next split's rows are in the plane)
+        const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(A.A1h + ((size_t)kt * A.a1_mpad + t0) * 32), 0, Mt * 64, 0x00020000);
+        st.ra[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rP, 16 * tid, 0, 0));
+      } else {
+        const float* Ap = s1 ? A.A1 : A.A0;
+        const __amdgpu_buffer_rsrc_t rA =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(Ap + (size_t)t0 * lda), 0, Mt * lda * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kR0AI; ++i) {
+          const int f = tid + i * kR0NT, r = f / (kR0BK / 4), kq = f % (kR0BK / 4);
+          const int vo = (k0 + kR0BK > K && k0 + 4 * kq >= K) ? kOob : (r * lda + 4 * kq) * 4;
+          st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, k0 * 4, 0));
+        }
+      }
       const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)(s1 ? A.B1 : A.B0), 0, bbytes,
                                                                           0x00020000);
 #pragma unroll
-      for (int i = 0; i < kR0AI; ++i) {
-        const int f = tid + i * kR0NT, r = f / (kR0BK / 4), kq = f % (kR0BK / 4);
-        const int vo = (k0 + kR0BK > K && k0 + 4 * kq >= K) ? kOob : (r * lda + 4 * kq) * 4;
-        st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, k0 * 4, 0));
-      }
-#pragma unroll
       for (int i = 0; i < kR0BI; ++i) {
+        if (pt && i >= kR0BI / 2) break;   // items [kR0BI / 2, kR0BI): the lo plane, unread on one product
         constexpr int CB = kR0BK / 8;   // 16-B chunks per column and k-tile
         const int f = tid + i * kR0NT, p = f / (256 * CB), rem = f % (256 * CB), n = rem / CB, kh = rem % CB;
         // columns past Npad and k past the planes' ldk (the next column's row) read 0
@@ -245,10 +263,13 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
         st.rb[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rB, vo, k0 * 2, 0));
       }
     };
-    auto sstore = [&](const Stage& st, int buf, bool s1) {
+    auto sstore = [&](const Stage& st, int buf, int t) {
       unsigned short* As = smem + buf * kR0STG;
       unsigned short* Bs = As + 2 * kR0APL;
-      const float sa = s1 ? sA1 : sA0;
+      const bool pt = sw && t < nk;
+      const float sa = (sw ? t < nk : t >= nk) ? sA1 : sA0;   // segment 1's scale (not read on pt)
+      if (pt) *reinterpret_cast<u16x8*>(As + swzk(tid >> 2, tid & 3)) = __builtin_bit_cast(u16x8, st.ra[0]);
+      else
 #pragma unroll
       for (int i = 0; i < kR0AI; ++i) {
         const int f = tid + i * kR0NT, r = f / (kR0BK / 4), kq = f % (kR0BK / 4);
@@ -266,6 +287,7 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       }
 #pragma unroll
       for (int i = 0; i < kR0BI; ++i) {
+        if (pt && i >= kR0BI / 2) break;
         constexpr int CB = kR0BK / 8;
         const int f = tid + i * kR0NT, p = f / (256 * CB), rem = f % (256 * CB);
         *reinterpret_cast<u16x8*>(Bs + p * kR0BPL + swzk(rem / CB, rem % CB)) = st.rb[i];
@@ -306,9 +328,9 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
 #pragma unroll
         for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{} + 1.0f;
     } else {
-      // segment 1's tiles on one product run as a second loop over [t1, ntiles) (t1 = nk, a multiple of the
-      // unroll; the loops' bodies differ only in the compute step -- a branch inside one loop spills)
-      const int t1 = (one1 && nk % R0_PF == 0) ? nk : ntiles;
+      // segment 1's one-product tiles [0, t1) and the 3-product tiles [t1, ntiles) as two loops (t1 a multiple
+      // of the unroll): their bodies differ in the compute step, and a branch there inside one loop spills
+      const int t1 = sw ? nk : 0;
 #if R0_PF == 4
       // four k-tiles of loads in flight: stage S_(j % 4) holds k-tile j from its load, issued three steps
       // ahead, until its LDS store
@@ -318,26 +340,26 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       gload(S1, cl(1));
       gload(S2, cl(2));
       gload(S3, cl(3));
-      sstore(S0, 0, false);
+      sstore(S0, 0, 0);
       lds_barrier();
       auto kloop = [&](int tb, int te, auto one_c) {
         for (int t = tb; t < te; t += 4) {
           // steps past the last k-tile (ntiles % 4 != 0) only keep the load pattern (uniform branches)
           gload(S0, cl(t + 4));
           compute(0, one_c);
-          if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
+          if (t + 1 < ntiles) sstore(S1, 1, t + 1);
           lds_barrier();
           gload(S1, cl(t + 5));
           if (t + 1 < ntiles) compute(1, one_c);
-          if (t + 2 < ntiles) sstore(S2, 0, t + 2 >= nk);
+          if (t + 2 < ntiles) sstore(S2, 0, t + 2);
           lds_barrier();
           gload(S2, cl(t + 6));
           if (t + 2 < ntiles) compute(0, one_c);
-          if (t + 3 < ntiles) sstore(S3, 1, t + 3 >= nk);
+          if (t + 3 < ntiles) sstore(S3, 1, t + 3);
           lds_barrier();
           gload(S3, cl(t + 7));
           if (t + 3 < ntiles) compute(1, one_c);
-          if (t + 4 < ntiles) sstore(S0, 0, t + 4 >= nk);
+          if (t + 4 < ntiles) sstore(S0, 0, t + 4);
           lds_barrier();
         }
       };
@@ -346,24 +368,27 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
       Stage S0, S1;
       gload(S0, 0);
       gload(S1, ntiles > 1 ? 1 : 0);
-      sstore(S0, 0, false);
+      sstore(S0, 0, 0);
       lds_barrier();
       auto kloop = [&](int tb, int te, auto one_c) {
         for (int t = tb; t < te; t += 2) {
           gload(S0, t + 2 < ntiles ? t + 2 : ntiles - 1);   // unconditional: keeps vmcnt counting exact
           compute(0, one_c);
-          if (t + 1 < ntiles) sstore(S1, 1, t + 1 >= nk);
+          if (t + 1 < ntiles) sstore(S1, 1, t + 1);
           lds_barrier();
           gload(S1, t + 3 < ntiles ? t + 3 : ntiles - 1);
           if (t + 1 < ntiles) compute(1, one_c);
-          if (t + 2 < ntiles) sstore(S0, 0, t + 2 >= nk);
+          if (t + 2 < ntiles) sstore(S0, 0, t + 2);
           lds_barrier();
         }
       };
 #endif
-      kloop(0, t1, std::false_type{});
-      __builtin_amdgcn_sched_barrier(0);
-      kloop(t1, ntiles, std::true_type{});
+      kloop(0, t1, std::true_type{});
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) acc[i][j] *= sDown;
+      kloop(t1, ntiles, std::false_type{});
     }
     if (kR0XAlias) {
       // the X image takes the staging buffers' bytes: every wave is past its last fragment read first
