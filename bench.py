@@ -175,7 +175,9 @@ def tag_bytes(tag: str, widths, n: int) -> float:
     elif role == "fvp_rbwd":
         cols = 2 * w[l + 1] + 4 * w[l]                      # RD_l, D_l ; H_l, E, RH_l ; RD_{l-1} out
     elif role == "fvp_rbwdwg":
-        cols = 2 * w[l + 1] + 3 * w[l] + w[l - 1]           # RD_l, D_l ; H_l, E, RH_l ; X (RD_{l-1} stays on chip)
+        # RD_l, D_l's f16 hi plane (the one-product D_l V_l^T segment; f32 D_l when the binade test does not
+        # fire -- it fires at C4) ; H_l, E, RH_l ; X (RD_{l-1} stays on chip)
+        cols = 1.5 * w[l + 1] + 3 * w[l] + w[l - 1]
     elif role == "pg_bwdwg":
         cols = w[l + 1] + w[l] + w[l - 1]                   # DS_l ; H_l ; X
     elif role == "fvp_tail":

@@ -128,13 +128,12 @@ __device__ __forceinline__ f32x16 mfma3h(const f16x8& ah, const f16x8& al, const
 }
 
 // NSEG = 2: FVP ([RD_1 | D_1], with the E RH term); NSEG = 1: policy gradient (DS_1, no E term)
-template <int NSEG>
-__global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
+// SW: segment 1 on one product from D_1's hi plane (decided per launch on the device, rbwd0_sw); the two
+// variants are separate instantiations so neither carries the other's live ranges
+template <int NSEG, bool SW>
+__device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* smem, float* sMax) {
   constexpr bool kE = NSEG == 2;
   constexpr int TM = kR0TM, CT = kR0CT;
-  __shared__ __attribute__((aligned(16))) unsigned short smem[kR0LDSU];
-  __shared__ float sMax[kR0NW];
-  if (A.skip && *A.skip) return;
 
   const int tid0 = threadIdx.x;
   const int r0 = blockIdx.x * A.rows_per_split;
@@ -168,7 +167,8 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   // 16-B load per thread and k-tile, half the bytes of f32 D_1). Its tiles run FIRST, at the plane's own
   // product scale 2^(eA1p + eB1); the accumulator then steps down to 2^eP (a power of two: exact) for
   // segment 0. Without the plane (or with a k-tile count the unrolled loop cannot split) both run 3 products.
-  const int sw = (kR0BK == 32 && NSEG > 1 && A.A1h && one1 && nk % R0_PF == 0) ? 1 : 0;
+  (void)one1;
+  constexpr int sw = SW ? 1 : 0;   // rbwd0_sw: one1 with the plane and an even split of the k-loop
   const int eA1p = sw ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;
   const float sDown = __builtin_ldexpf(1.0f, sw ? eP - (eA1p + eB1) : 0);
   const int bbytes = (int)(2 * A.plane * 2);
@@ -542,6 +542,29 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
     const float bt = xadd_f<true>(bsum[tn]);   // the two lane halves' rows, same order on both
     if (lh == 0 && j < A.N) out[A.off_b + j] = bt;
   }
+}
+
+__device__ __forceinline__ bool rbwd0_sw(const RBwd0Args& A) {
+  if (kR0BK != 32 || A.nseg < 2 || !A.A1h || A.low_seg <= 0) return false;
+  const int nk = (A.K + kR0BK - 1) / kR0BK;
+  if (nk % R0_PF) return false;
+  const int q0 = amax_exp(A.am_a0) + amax_exp(A.am_b0), q1 = amax_exp(A.am_a1) + amax_exp(A.am_b1);
+  const int pen0 = (!A.am_a0 || !A.am_b0) ? 4 : 0;
+  return __builtin_amdgcn_readfirstlane(q1 - q0 >= A.low_seg + pen0 ? 1 : 0) != 0;
+}
+
+template <int NSEG>
+__global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[kR0LDSU];
+  __shared__ float sMax[kR0NW];
+  if (A.skip && *A.skip) return;
+  if constexpr (NSEG > 1) {
+    if (rbwd0_sw(A)) {
+      rbwd0_body<NSEG, true>(A, smem, sMax);
+      return;
+    }
+  }
+  rbwd0_body<NSEG, false>(A, smem, sMax);
 }
 
 }  // namespace
