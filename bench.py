@@ -206,6 +206,20 @@ def tail_used(widths) -> bool:
     return 128 < a <= 256 and a % 32 == 0 and 16 < b <= 32 and widths[L] <= 32
 
 
+def tag_x_bytes(tag: str, widths, n: int) -> float:
+    """SURVEY.md §8(d)'s algorithmic bytes of one launch: the states' X rows (N*obs*4) when the kernel
+    reads X, else 0 (every other operand is an intermediate the algorithm need not materialise)."""
+    if tag in ("fvp_chain", "fvp_fused"):
+        return 4.0 * n * widths[0]
+    role, _, l = tag.rpartition("_l")
+    if not l.isdigit():
+        return 0.0
+    l = int(l)
+    reads_x = (l == 0 and role in ("fvp_rfwd", "fvp_wgrad", "fwd", "ls_fwd", "pg_wgrad")) or \
+        (l == 1 and role in ("fvp_rbwdwg", "pg_bwdwg"))
+    return 4.0 * n * widths[0] if reads_x else 0.0
+
+
 def tag_roof(tag: str, widths, n: int):
     """(bound, seconds at the roof) of one launch."""
     t_mfma = tag_flops(tag, widths, n) / (tag_peak(tag, widths) * 1e12)
@@ -222,7 +236,7 @@ def committed_traffic(config: str, rows: int, tag: str):
         except (OSError, ValueError):
             continue
         if d.get("config") == config and d.get("rows") == rows and tag in d.get("tags", {}):
-            best = (os.path.relpath(f, ROOT), d["tags"][tag])
+            best = (os.path.relpath(f, ROOT), d["tags"][tag], d.get("build"))
     return best
 
 
@@ -422,6 +436,34 @@ def comm_block(eng, world, rank, rehearsal, dist):
             "world": world, "distinct_devices": len(set(buses)), "per_rank": ranks}
 
 
+def launch_ranks(argv, gpus: int, rehearsal: bool, visible_gpus: int) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N ranks on this node as one child
+    process (`python -m torch.distributed.run`, rendezvous on 127.0.0.1), relay their output and return
+    the launcher's exit status (non-zero when any rank fails).  Nothing here touches the GPU: the parent
+    only counts devices, then waits.  More ranks than visible GPUs is refused unless --rehearsal."""
+    import socket
+    import subprocess
+    if gpus > visible_gpus and not rehearsal:
+        sys.stderr.write(f"bench.py: --gpus {gpus} but {visible_gpus} GPU(s) visible; "
+                         f"pass --rehearsal to let ranks share GPUs\n")
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", "--max-restarts=0",
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def visible_gpu_count() -> int:
+    """Devices this process could use, counted without initialising the GPU runtime."""
+    import torch
+    return torch.cuda.device_count()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -440,6 +482,11 @@ def main():
                     help="at one rank, still create a (one-rank) RCCL communicator: every all-reduce runs "
                          "through RCCL, and the comm block records it")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's form `python bench.py --gpus N`: become the launcher of N ranks
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus, args.rehearsal, visible_gpu_count()))
 
     cfg = dict(CONFIGS[args.config])
     if args.rows:
@@ -449,7 +496,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if world != args.gpus and world > 1:
+    if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
@@ -535,6 +582,7 @@ def main():
         avg_s = tot_ms / cnt / 1e3
         fl = tag_flops(dom, widths, n)
         by = tag_bytes(dom, widths, n)
+        alg_by = tag_x_bytes(dom, widths, n)
         peak = tag_peak(dom, widths)
         achieved = fl / avg_s / 1e12
         bound, _ = tag_roof(dom, widths, n)   # max(own bytes / HBM peak, FLOPs / MFMA peak)
@@ -589,31 +637,28 @@ def main():
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce of [P] FVP/grad + loss scalars)"
                        if not rehearsal or world == 1 else
                        f"dp{world} on {ndev} GPU(s): rehearsal, ranks share GPUs, gloo host all-reduce"},
-            "roofline": {"bound": bound, "kernel": dom,
-                         "achieved": by / avg_s / 1e9 if bound == "hbm" else achieved,
-                         "peak": PEAK_HBM_GBS if bound == "hbm" else peak,
-                         "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
-                         "frac": (by / avg_s / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else achieved / peak,
+            "roofline": {"bound": "mfma", "kernel": dom,
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": tr[1]["traffic_bytes"] if tr else None,
-                         "bound_basis": "the larger of the launch's own operand bytes / 8 TB/s and its FLOPs / "
-                                        "the split MFMA peak (bench.tag_roof)",
-                         "achieved_basis": ("algorithmic bytes of this launch (each activation operand read once, "
-                                            "each output written once, f32) / its average launch time"
-                                            if bound == "hbm" else
-                                            "SURVEY.md §8(d) algorithmic FLOPs of this kernel's share of the FVP "
-                                            "(4ab R-forward / 4ab R-backward / 4ab weight-R-gradient per state and "
-                                            "layer) / its average launch time"),
-                         "mfma_achieved_tflops": achieved, "mfma_peak_tflops": peak, "mfma_frac": achieved / peak,
+                         "bound_basis": "SURVEY.md §8(d): the FVP is compute-bound at every config (arithmetic "
+                                        "intensity >= 187 flop/B of algorithmic bytes)",
+                         "achieved_basis": "SURVEY.md §8(d) algorithmic FLOPs of this kernel's share of the FVP "
+                                           "(4ab R-forward / 4ab R-backward / 4ab weight-R-gradient per state and "
+                                           "layer, 2ab for layer 1's R-forward and weight R-gradient) / its average "
+                                           "launch time (HIP events on the engine stream)",
                          "peak_basis": peak_basis,
                          "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt,
+                         "algorithmic_bytes_per_launch": alg_by,
+                         "algorithmic_bytes_frac": alg_by / avg_s / 1e9 / PEAK_HBM_GBS,
+                         "own_bound": bound,
                          "own_traffic_bytes_per_launch": by,
                          "own_traffic_hbm_gbs": by / avg_s / 1e9,
                          "own_traffic_hbm_frac": by / avg_s / 1e9 / PEAK_HBM_GBS,
                          "hbm_gbs_at_traffic": tr[1]["traffic_bytes"] / avg_s / 1e9 if tr else None,
                          "traffic_source": tr[0] if tr else None,
-                         "traffic_build": tr[1].get("build") if tr else None,
+                         "traffic_build": tr[2] if tr else None,
                          "build": source_build_id(),
-                         "traffic_same_build": bool(tr and tr[1].get("build") == source_build_id())},
+                         "traffic_same_build": bool(tr and tr[2] == source_build_id())},
             "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
                                 "achieved_tflops": upd_flops * world / upd_s / 1e12,
                                 "roof_ms_per_update": upd_peak_s * 1e3,

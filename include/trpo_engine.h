@@ -94,9 +94,10 @@ void* trpo_stream(trpo_engine* e);
  * FVP / gradient / loss sums of each rank's shard are all-reduced. */
 int trpo_comm_unique_id(uint8_t out_id[128]);
 int trpo_comm_init(trpo_engine* e, const uint8_t id[128], int rank, int world);
-/* Test transport: instead of RCCL, every all-reduce syncs the stream, copies the buffer to host
- * and calls cb(host_buf, count, dtype = TRPO_F32 / TRPO_F64, ctx), which must sum it across ranks
- * in place (e.g. torch.distributed over gloo).  Lets several ranks share one GPU in tests. */
+/* Test transport: instead of RCCL, every all-reduce is stream-ordered and capturable: an async copy of
+ * the buffer into a pinned host slot, a hipLaunchHostFunc callback that calls cb(host_buf, count,
+ * dtype = TRPO_F32 / TRPO_F64, ctx), which must sum it across ranks in place (e.g. torch.distributed
+ * over gloo), and an async copy back.  Lets several ranks share one GPU in tests. */
 typedef int (*trpo_allreduce_cb)(void* host_buf, int64_t count, int dtype, void* ctx);
 int trpo_comm_set_host_allreduce(trpo_engine* e, trpo_allreduce_cb cb, void* ctx, int rank, int world);
 /* What carries this engine's all-reduces, for a launcher to verify (e.g. that N ranks of an RCCL

@@ -1,0 +1,71 @@
+"""bench.py's multi-rank launch logic (CPU only: no rank ever reaches the GPU here).
+
+`python bench.py --gpus N` without WORLD_SIZE must start N ranks itself (the driver's scaling run uses
+that form), refuse more ranks than visible GPUs unless --rehearsal, and print no JSON line when it
+refuses.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _env_without_world():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    return env
+
+
+def test_more_ranks_than_gpus_fails_cleanly():
+    # this container has no GPU: --gpus 8 must exit non-zero before any GPU work, with no JSON line
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], cwd=ROOT,
+                       env=_env_without_world(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
+    for line in r.stdout.splitlines():
+        with pytest.raises(ValueError):
+            json.loads(line)
+
+
+def test_launcher_command(monkeypatch):
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    rc = bench.launch_ranks(["--gpus", "4", "--steps", "2"], 4, False, visible_gpus=8)
+    assert rc == 7                                  # the launcher's status is the parent's exit status
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"]
+    assert cmd[-5].endswith("bench.py")
+    assert any(c.startswith("--master-port=") and int(c.split("=")[1]) > 0 for c in cmd)
+
+
+def test_launcher_refuses_without_rehearsal(monkeypatch):
+    monkeypatch.setattr(subprocess, "call", lambda *a, **k: pytest.fail("must not launch"))
+    assert bench.launch_ranks(["--gpus", "2"], 2, False, visible_gpus=1) != 0
+
+
+def test_launcher_rehearsal_allows_shared_gpus(monkeypatch):
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: 0)
+    assert bench.launch_ranks(["--gpus", "2", "--rehearsal"], 2, True, visible_gpus=1) == 0
+
+
+def test_world_size_mismatch_is_refused():
+    env = _env_without_world()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -19,9 +19,11 @@
 //     4 rows 16s + 8t + 4h .. +3 of column m, the matching A operand.  The image arrives by LDS-DMA
 //     (buffer_load ... lds) at the start of each tile, overlapped with the k-loop.
 //   * k-loop: the register-staged f16 split of rowgemm3_kernel (A split on the way to LDS, B from the
-//     engine's pre-split weight planes), BK = 16, two k-tiles of loads in flight.
-//   * Scales: the row GEMM's two segments share one product scale (the smaller of their running-max ones,
-//     so one 3-product k-loop covers both); X from its planes' exponent; RD_0 per
+//     engine's pre-split weight planes), BK = 32 (R0_BK), two k-tiles of loads in flight.
+//   * Scales: when segment 1 (D_1 V_1^T) sits >= low_seg binades under segment 0 (rbwd0_sw, the C4 case) its
+//     tiles run first on one product from D_1's f16 hi plane at the plane's own scale, and the accumulator
+//     then steps down by an exact power of two to segment 0's; otherwise the two segments share one product
+//     scale (the smaller of their running-max ones) on three products.  X from its planes' exponent; RD_0 per
 //     tile (workgroup max), the weight-gradient accumulator rescaled (exactly, by a power of two) whenever a
 //     tile needs a smaller exponent than the running one, and unscaled once at the end.
 #include "rowepi.h"
@@ -231,9 +233,11 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
     };
     // tile t: segment 1 is tiles [0, nk) under sw, [nk, 2 nk) otherwise; pt = a D_1 hi-plane tile
     auto gload = [&](Stage& st, int t) {
+      // segment 1 exists only for NSEG == 2 (compile time): a one-segment launch never forms an A1 / B1
+      // address, whatever tile index reaches here
       const bool pt = sw && t < nk;
-      const bool s1 = sw ? t < nk : t >= nk;
-      const int kt = t >= nk ? t - nk : t;
+      const bool s1 = NSEG > 1 && (sw ? t < nk : t >= nk);
+      const int kt = (NSEG > 1 && t >= nk) ? t - nk : t;
       const int k0 = kt * kR0BK;
       if (pt) {
         // rows past the tile's Mt read 0 (the next split's rows are in the plane)
@@ -267,7 +271,7 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
       unsigned short* As = smem + buf * kR0STG;
       unsigned short* Bs = As + 2 * kR0APL;
       const bool pt = sw && t < nk;
-      const float sa = (sw ? t < nk : t >= nk) ? sA1 : sA0;   // segment 1's scale (not read on pt)
+      const float sa = (NSEG > 1 && (sw ? t < nk : t >= nk)) ? sA1 : sA0;   // segment 1's scale (not read on pt)
       if (pt) *reinterpret_cast<u16x8*>(As + swzk(tid >> 2, tid & 3)) = __builtin_bit_cast(u16x8, st.ra[0]);
       else
 #pragma unroll
@@ -585,6 +589,12 @@ void launch_rbwd0(const RBwd0Args& a, hipStream_t s) {
   if ((a.nseg == 2) != (a.E != nullptr)) throw std::runtime_error("rbwd0: the E RH term goes with two segments");
   RBwd0Args b = a;
   b.low_seg = g_options.low_seg;
+  if (b.nseg == 1) {   // no absent operand is ever a null base: segment 1 aliases segment 0 (never read)
+    b.A1 = b.A0;
+    b.B1 = b.B0;
+    b.am_a1 = b.am_a0;
+    b.am_b1 = b.am_b0;
+  }
   if (a.nseg == 2) hipLaunchKernelGGL(rbwd0_kernel<2>, dim3(a.splits), dim3(kR0NT), 0, s, b);
   else hipLaunchKernelGGL(rbwd0_kernel<1>, dim3(a.splits), dim3(kR0NT), 0, s, b);
 }
