@@ -114,10 +114,6 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return ab + 2.0 * n * widths[l - 1] * widths[l]
     if role == "fvp_tail":          # fused last layer: R-forward (2ab) + R-backward (2ab) + weight R-gradient (2ab)
         return 6 * ab
-    if role == "fvp_head":          # R-forward (2ab) + R-backward (2ab) + wgrad (2ab) of the last layer
-        return 3 * ab
-    if role == "fvp_headbwd":       # R-backward (2ab) + wgrad (2ab) of the last layer
-        return 2 * ab
     return 0.0
 
 
@@ -134,8 +130,6 @@ def tag_is_split(tag: str, widths) -> bool:
     a, b = pad(widths[l]), pad(widths[l + 1])
     if role.endswith("wgrad"):
         return get_option("split_wg") != 0 and b > 128
-    if role in ("fvp_head", "fvp_headbwd"):
-        return False
     if role in ("fvp_tail", "fvp_rbwdwg", "pg_bwdwg"):   # tail.hip / rbwd0.hip: always the f16 hi+lo split
         return True
     last = l == len(widths) - 2

@@ -188,11 +188,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
                   double* out, int mem);
 
 /* ---- kernel-variant switches (for A/B measurements and variant parity tests) ----------
- * "row_cfg" (wide f32 row-GEMM tile, 0..5), "wg_cfg" (weight-gradient tile, 0..1),
- * "narrow_pf" (prefetch depth of the narrow tiles, 1..2), "split_mfma" (0 = f32 MFMA row GEMMs;
- * 1..7 = split-bf16 row-GEMM tile for outputs wider than 128), "split_wg" (0 = f32 weight
- * gradients; 1..3 = split-bf16 tile for fan_out > 128), "fused_head" and "head_bwd"
- * (last-layer fusions; read when an engine is created), "chain" (fused FVP chain: 0 off, 1 auto),
+ * "split_mfma" (0 = f32 MFMA row GEMMs; 5 = the 256 x 256 split row-GEMM tile for outputs wider than
+ * 128, the default; any other value = the 128 x 256 tile), "split_wg" (0 = f32 weight gradients;
+ * 1 = split tile for fan_out > 128), "chain" (fused FVP chain: 0 off, 1 auto, 2..4 forced variants),
  * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
  * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph, all-reduces
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
@@ -204,16 +202,13 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * f16 product instead of three; 4 more binades when the dominant segment has an operand without a
  * running max; 0 = off; default 14), "planes" (1 = row GEMMs whose operands the engine keeps as
  * pre-split k-blocked f16 hi/lo planes run the LDS-DMA plane kernel of plane.hip; bit-identical to
- * the register-staged split; default 1), "e16" (1 = the tanh'' terms E_l that the per-layer R-backward
- * row GEMMs read are stored as the 16-bit high and low halves of each f32 word; the R-backward reads
- * both halves (the f32 value, bit for bit) or, when the E RH term's running-max product scale lies
- * low_seg + 3 binades below the main term's, the high halves alone; default 0: at C4 the test does not fire and the two 16-bit loads cost more than one f32 load),
+ * the register-staged split; default 1),
  * "rbwd0" (1 = layer 1's R-backward and layer 0's weight gradient run as one launch of rbwd0.hip:
  * RD_0 stays in registers and X^T RD_0 is reduced from the engine's X planes; eligible on the f16
  * split with planes on, obs <= 128, hidden widths <= 256 and multiples of 32; also serves the policy
- * gradient's layer-1 backward; default 1), "dual" (1 = the FVP's layer-1 weight gradient runs on a
- * second stream beside the fused R-backward, joined by events and capturable in the update graph;
- * needs rbwd0, the fused tail and two hidden layers; default 0: slower at C4).
+ * gradient's layer-1 backward; default 1).
+ * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed
+ * from the build in round 4; tools/patches/pruned_variants.patch restores them.
  * Process-wide. */
 int trpo_set_option(const char* name, int value);
 int trpo_get_option(const char* name, int* value);

@@ -89,8 +89,8 @@ def test_learn_matches_oracle_loop(gpu_available):
     device's action_dists under the same uniforms), so per-iteration numbers compare on identical
     paths; its own policy on those states must match the device's dists.  Bars: paths, actions,
     starts, rewards exact; returns 1e-12; baselines / advantages 1e-4 (the float32 VF after 50 Adam
-    steps, tests/test_gpu_vf.py); k exact; surr / kl / ent / explained variance 1e-4 relative at iteration 0
-    (zero baseline, no VF in the loop), 1e-3 after (the VF's advantage drift)."""
+    steps, tests/test_gpu_vf.py); k exact; surr / kl / ent / explained variance 1e-5 relative at iteration 0
+    (zero baseline, no VF in the loop: north_star's bar), 1e-3 after (the VF's advantage drift)."""
     from trpo_amd import TRPOAgent
     from oracle import learn_oracle
     draws = _draws(11, N_ITER)
@@ -117,7 +117,7 @@ def test_learn_matches_oracle_loop(gpu_available):
         assert rel_l2(h["advantages"], r["advantages"]) < 1e-4, (i, rel_l2(h["advantages"], r["advantages"]))
         assert h["k"] == r["k"] and h["reverted"] == r["reverted"], (i, h["k"], r["k"])
         # iteration 0 has no VF in the loop (zero baseline): only the update's own arithmetic separates the two
-        rel = 1e-4 if i == 0 else 1e-3
+        rel = 1e-5 if i == 0 else 1e-3
         for key in ("surr", "kl", "ent", "explained_variance"):
             hk = "entropy" if key == "ent" else key
             assert h[hk] == pytest.approx(r[hk], rel=rel, abs=1e-7), (i, key, h[hk], r[hk])

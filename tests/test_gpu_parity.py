@@ -270,24 +270,16 @@ def test_bad_actions_fail_loudly(gpu_available):
 @pytest.mark.parametrize("opts", [
     {"chain": 2}, {"chain": 3},               # fused FVP chain forms (default 1 = auto)
     {"chain": 0},                               # per-layer row-GEMM FVP
-    {"chain": 0, "fused_head": 1},     # LDS-resident last-layer fusion (opt-in)
-    {"chain": 0, "head_bwd": 1},       # last-layer R-backward + wgrad in one kernel (opt-in)
-    {"narrow_pf": 2},                  # two-stage prefetch for the narrow memory-bound tiles
-    {"row_cfg": 1}, {"row_cfg": 2}, {"row_cfg": 3}, {"row_cfg": 4}, {"row_cfg": 5},
-    {"wg_cfg": 1},
-    {"split_mfma": 0}, {"chain": 0, "split_mfma": 1}, {"chain": 0, "split_mfma": 2}, {"split_mfma": 3},
-    {"split_mfma": 4}, {"chain": 0, "split_mfma": 5}, {"chain": 0, "split_mfma": 6}, {"split_mfma": 7},
-    {"split_wg": 0}, {"split_wg": 1}, {"split_wg": 2}, {"split_wg": 3},
+    {"split_mfma": 0}, {"chain": 0, "split_mfma": 1}, {"chain": 0, "split_mfma": 5},
+    {"split_wg": 0}, {"split_wg": 1},
     {"split_mfma": 5, "split_wg": 1},
-    {"split_mfma": 8}, {"split_mfma": 9},                     # 128 x 256, two blocks per CU
-    {"split_mfma": 10}, {"split_mfma": 11},                   # 256 x 256, LDS-DMA ring / BK 32
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
     {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
     {"low_seg": 0}, {"low_seg": 0, "chain": 0},               # every split segment on three products
     {"planes": 0},                                            # register-staged split instead of the plane kernel
-    {"e16": 1, "rbwd0": 0}, {"e16": 1, "chain": 0, "rbwd0": 0},  # E_l as 16-bit high / low planes
+    {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
@@ -295,9 +287,8 @@ def test_kernel_variants_parity(gpu_available, opts):
     C1 dims, plus a 256-wide case that exercises the wide row-GEMM tiles and the widest chain."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
-    defaults = {k: get_option(k) for k in ("fused_head", "head_bwd", "row_cfg", "wg_cfg", "narrow_pf", "split_mfma",
-                                           "split_wg", "chain", "split_f16", "split_min_k", "fused", "low_seg",
-                                           "planes", "e16", "rbwd0")}
+    defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
+                                           "low_seg", "planes", "tail", "rbwd0")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -759,62 +750,6 @@ def test_flatgrad_of_gvp_is_the_fvp(gpu_available):
                                  float(d["residual_tol"]))
     assert_vec_close(stepdir, d["stepdir"], REL, "CG over the flatgrad(gvp) operator")
     eng.close()
-
-
-@pytest.mark.parametrize("obs,hidden,A,n", [(128, [256, 256], 18, 3001), (37, [200, 264, 144], 5, 1337),
-                                            (128, [256, 256, 256], 18, 2000)], ids=["c4_dims", "odd_wide", "depth3"])
-def test_e16_planes_exact_and_truncated(gpu_available, obs, hidden, A, n):
-    """E_l (the tanh'' term of the R-backward, trpo_inksci.py:56-70 through SURVEY.md Appendix A) kept as
-    the 16-bit high / low halves of each f32 word (option e16, RowEpi::kRBwd16).  With low_seg = 0 the
-    R-backward reads both halves: FVP, gradient and update are bit-identical to f32 E.  With the default
-    binade test the high halves alone may be read; the results must stay on the float64 oracle at 1e-5,
-    and re-preparing after an e16 switch must give the same bits as a fresh engine."""
-    from trpo_amd import Engine, UpdateParams
-    from trpo_amd._lib import get_option, set_option
-    spec = O.PolicySpec(obs, hidden, A)
-    d = O.synthetic_batch(spec, n, seed=41)
-    v = np.random.RandomState(42).standard_normal(spec.n_params).astype(np.float32)
-    saved = {k: get_option(k) for k in ("e16", "low_seg", "rbwd0")}
-    set_option("rbwd0", 0)   # the fused layer-1 R-backward reads f32 E (use_e16 is off under it)
-
-    def run(e16, low_seg):
-        set_option("e16", e16)
-        set_option("low_seg", low_seg)
-        eng = Engine(obs, hidden, A, max_rows=n + 100)
-        eng.set_flat(d["theta"])
-        eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
-        hv, g = eng.fvp(v, 0.0), eng.policy_grad()
-        st = eng.update(UpdateParams(cg_iters=10, residual_tol=0.0))
-        th = eng.get_flat()
-        eng.close()
-        return hv, g, th, st
-
-    try:
-        a, b = run(0, 0), run(1, 0)
-        for i, what in enumerate(("Hv", "g", "theta")):
-            np.testing.assert_array_equal(a[i], b[i], err_msg=f"e16 exact {what}")
-        t = run(1, 14)
-        ref = O.fvp_undamped(d["theta"].astype(np.float64), d["X"], v.astype(np.float64), spec)
-        assert_vec_close(t[0], ref, REL, "Hv, e16 with the high-half test")
-        r = O.trpo_update(d["theta"].astype(np.float64), O.Batch(d["X"], d["actions"], d["advant"], d["old_dist"]),
-                          spec, np.float64, 10, 0.0)
-        assert t[3]["k"] == r.k
-        assert_vec_close(t[2], r.theta_new, REL, "theta, e16 with the high-half test")
-        # one engine switched between the forms after prepare() re-prepares (engine.cpp fvp(), prep_e16)
-        set_option("low_seg", 0)
-        set_option("e16", 1)
-        eng = Engine(obs, hidden, A, max_rows=n + 100)
-        eng.set_flat(d["theta"])
-        eng.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
-        h1 = eng.fvp(v, 0.0)
-        set_option("e16", 0)
-        h0 = eng.fvp(v, 0.0)
-        eng.close()
-        np.testing.assert_array_equal(h1, b[0])
-        np.testing.assert_array_equal(h0, a[0])
-    finally:
-        for k, val in saved.items():
-            set_option(k, val)
 
 
 @pytest.mark.parametrize("obs,hidden,A,n", [

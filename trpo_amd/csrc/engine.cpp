@@ -40,10 +40,6 @@ struct trpo_engine {
   int device = 0;
   int num_cus = 256;               // compute units of `device` (hipDeviceAttributeMultiprocessorCount)
   hipStream_t stream = nullptr;
-  // second stream for the FVP's weight gradients, which run beside the R-backward (option dual); joined
-  // back into `stream` by events, so the pattern is capturable
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // policy shape
   int L = 0;                       // layers
   std::vector<int> w, wp;          // widths [obs, hidden..., A] and padded
@@ -105,7 +101,6 @@ struct trpo_engine {
   unsigned* am_ds(int l) const { return am(4, l); }
   unsigned* am_rh(int l) const { return am(5, l); }
   unsigned* am_rd(int l) const { return am(6, l); }
-  unsigned* am_e(int l) const { return am(7, l); }
   void am_reset(unsigned* first, int count) {
     if (first && count > 0)
       HIPCHECK(hipMemsetAsync(first, 0, (size_t)count * kAmaxSlot * sizeof(unsigned), stream));
@@ -144,22 +139,13 @@ struct trpo_engine {
   uint16_t* tail_planes = nullptr;   // head planes of the fused FVP tail (tail.hip), [2][2][32][kTailK]
   // the fused last-layer tail: f16 split, last hidden width in (128, 256], 17..32 actions
   bool use_tail() const {
-    return g_options.tail != 0 && f16 && split_on() && L >= 2 && !fused_head && !head_bwd &&
+    return g_options.tail != 0 && f16 && split_on() && L >= 2 &&
            tail_eligible(wp[L - 1], wp[L]) && w[L] <= 32;
   }
   // whether the FVP path reads E_{L-2} (the plain tanh'' term under the last hidden layer): every path
   // but the fused tail, which recomputes it (tail.hip)
   bool e_top_needed() const { return L < 2 || !use_tail() || use_fused() || use_chain(); }
   bool prep_e_top = true;    // prepare() wrote E_{L-2}
-  // E_l as 16-bit high/low planes (RowEpi::kRBwd16) wherever the per-layer R-backward row GEMMs read them:
-  // every path but the chain / one-launch FVP and the opt-in last-layer fusions, which read f32 E
-  bool use_e16() const {
-    return g_options.e16 != 0 && !use_chain() && !use_fused() && !fused_head && !head_bwd && !use_rbwd0();
-  }
-  bool prep_e16 = false;     // prepare() wrote E in that form
-  int64_t e16_lo(int l) const { return cap * wp[l + 1]; }   // u16 offset of E_l's low-half plane
-  bool fused_head = false;   // last layer's R-forward + R-backward + wgrad in one kernel (opt-in)
-  bool head_bwd = false;     // last layer's R-backward + wgrad in one kernel (default)
 
   // fused FVP chain (chain.hip): weight images in consumption order + chunk table
   int chain_otm = 0;         // register tiles per hidden layer; 0 = shape not eligible
@@ -310,9 +296,6 @@ struct trpo_engine {
     use();
     HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    HIPCHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    HIPCHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    HIPCHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     w.push_back(obs);
     for (int i = 0; i < nh; ++i) w.push_back(hidden[i]);
     w.push_back(A);
@@ -390,9 +373,6 @@ struct trpo_engine {
     sc = dalloc<UpdScalars>(1);
     fl = dalloc<CGFlags>(1);
     dbad = dalloc<int>(1);
-    fused_head = L >= 2 && wp[L - 1] <= 256 && wp[L - 1] % 16 == 0 && wp[L] <= 32 &&
-                 g_options.fused_head != 0;   // opt-in: slower than the split kernels at C4 (1 block/CU)
-    head_bwd = !fused_head && L >= 2 && wp[L - 1] <= 256 && wp[L] <= 32 && g_options.head_bwd != 0;
     f16 = g_options.split_f16 != 0;
     amax = dalloc<unsigned>((size_t)(1 + 8 * kMaxLayers) * kAmaxSlot);
     if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
@@ -601,10 +581,6 @@ struct trpo_engine {
     free_har_slots();
     if (hsc) (void)hipHostFree(hsc);
     if (comm) (void)ncclCommDestroy(comm);
-    if (side) (void)hipStreamSynchronize(side);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -873,8 +849,6 @@ struct trpo_engine {
     // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
     // recomputes it from H and D_{L-1}.
     prep_e_top = e_top_needed();
-    prep_e16 = use_e16();
-    am_reset(am_e(0), L);
     for (int l = L - 1; l >= 1; --l) {
       const bool need_d = l > 1, need_e = l < L - 1 || prep_e_top;
       if (!need_d && !need_e) continue;
@@ -885,15 +859,11 @@ struct trpo_engine {
       a.seg[0].amaxA = am_d(l);
       a.seg[0].amaxB = am_w(l);
       // both: kPrepBwd ; E only (D_0): kPrepBwdE ; D only: kPgBwd, whose epilogue is DH (1-H^2)
-      // (E as 16-bit planes: kPrepBwd16 / kPrepBwdE16, with its running max for the R-backward's test)
-      a.epi = need_d ? (need_e ? (prep_e16 ? RowEpi::kPrepBwd16 : RowEpi::kPrepBwd) : RowEpi::kPgBwd)
-                     : (prep_e16 ? RowEpi::kPrepBwdE16 : RowEpi::kPrepBwdE);
+      a.epi = need_d ? (need_e ? RowEpi::kPrepBwd : RowEpi::kPgBwd) : RowEpi::kPrepBwdE;
       a.ea.H = H[l];
       a.ea.out0 = need_d ? D[l - 1] : E[l - 1];
-      a.ea.amax0 = need_d ? am_d(l - 1) : (prep_e16 ? am_e(l - 1) : nullptr);
+      a.ea.amax0 = need_d ? am_d(l - 1) : nullptr;
       a.ea.out1 = need_d && need_e ? E[l - 1] : nullptr;
-      a.ea.amax1 = need_d && need_e && prep_e16 ? am_e(l - 1) : nullptr;
-      a.ea.e16_lo = e16_lo(l - 1);
       a.ea.ldo = wp[l];
       char t[32];
       std::snprintf(t, sizeof t, "bwd_l%d", l);
@@ -998,8 +968,8 @@ struct trpo_engine {
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
   void fvp(const float* v, float* out, const int* skip) {
-    // the path changed since prepare(): E_{L-2} needed but not written, or E in the other form
-    if (prepared && ((e_top_needed() && !prep_e_top) || prep_e16 != use_e16())) prepared = false;
+    // the path changed since prepare(): E_{L-2} needed but not written
+    if (prepared && e_top_needed() && !prep_e_top) prepared = false;
     prepare();
     if (use_fused()) {
       fvp_fused(v, out, skip);
@@ -1020,7 +990,7 @@ struct trpo_engine {
     am_reset(am_rd(0), L);
     // R-forward (the fused tail takes the last layer's)
     const bool tail = use_tail();
-    const int Lf = (fused_head || tail) ? L - 1 : L;
+    const int Lf = tail ? L - 1 : L;
     for (int l = 0; l < Lf; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       float* Vpart = WF[l] + (size_t)wp[l] * wp[l + 1];
@@ -1063,67 +1033,6 @@ struct trpo_engine {
       Scope sp(this, tag);
       launch_rowgemm(a, stream);
       check_launch();
-    }
-    if (fused_head) {
-      HeadArgs h{};
-      const int l = L - 1;
-      h.rows = (int)n;
-      h.a = w[l];
-      h.b = w[l + 1];
-      h.apad = wp[l];
-      h.bpad = wp[l + 1];
-      h.RH = RH[l];
-      h.H = H[l];
-      h.WF = WF[l];
-      h.WB = WB[l];
-      h.c = v + offb[l];
-      h.P = Pm;
-      h.DL = D[l];
-      h.E = E[l - 1];
-      h.RDout = RD[l - 1];
-      h.invN = 1.0 / (double)n_global;
-      h.splits = active_splits;
-      h.rows_per_split = rows_per_split;
-      h.slab = slab;
-      h.slab_stride = slab_stride;
-      h.off_w = offW[l];
-      h.off_b = offb[l];
-      h.skip = skip;
-      char tag[32];
-      std::snprintf(tag, sizeof tag, "fvp_head_l%d", l);
-      Scope sp(this, tag);
-      launch_fvp_head(h, stream);
-      check_launch();
-      if (f16) launch_amax(RD[l - 1], n, w[l], wp[l], am_rd(l - 1), stream);
-    }
-    if (head_bwd) {
-      HeadBwdArgs h{};
-      const int l = L - 1;
-      h.rows = (int)n;
-      h.a = w[l];
-      h.b = w[l + 1];
-      h.apad = wp[l];
-      h.bpad = wp[l + 1];
-      h.RH = RH[l];
-      h.H = H[l];
-      h.E = E[l - 1];
-      h.WB = WB[l];
-      h.RDL = RD[l];
-      h.DL = D[l];
-      h.RDout = RD[l - 1];
-      h.splits = active_splits;
-      h.rows_per_split = rows_per_split;
-      h.slab = slab;
-      h.slab_stride = slab_stride;
-      h.off_w = offW[l];
-      h.off_b = offb[l];
-      h.skip = skip;
-      char tag[32];
-      std::snprintf(tag, sizeof tag, "fvp_headbwd_l%d", l);
-      Scope sp(this, tag);
-      launch_head_bwd(h, stream);
-      check_launch();
-      if (f16) launch_amax(RD[l - 1], n, w[l], wp[l], am_rd(l - 1), stream);
     }
     if (tail) {
       const int l = L - 1;
@@ -1173,7 +1082,7 @@ struct trpo_engine {
       launch_fvp_tail(ta, stream);
       check_launch();
     }
-    const bool tail_fused = fused_head || head_bwd || tail;
+    const bool tail_fused = tail;
     // layer 1's R-backward fused with layer 0's weight gradient when layer 1 is not inside the tail
     const bool r0f = use_rbwd0() && (tail_fused ? L - 2 : L - 1) >= 1;
     auto r_backward = [&]() {
@@ -1209,12 +1118,9 @@ struct trpo_engine {
         a.seg[1].amaxA = am_d(l);
         a.seg[1].amaxB = am_v(l);
         a.skip = skip;
-        a.epi = prep_e16 ? RowEpi::kRBwd16 : RowEpi::kRBwd;
+        a.epi = RowEpi::kRBwd;
         a.ea.H = H[l];
         a.ea.E = E[l - 1];
-        a.ea.e16_lo = e16_lo(l - 1);
-        a.ea.amaxE = am_e(l - 1);
-        a.ea.amaxRH = am_rh(l);
         a.ea.RH = RH[l];
         a.ea.out0 = RD[l - 1];
         a.ea.amax0 = am_rd(l - 1);
@@ -1238,22 +1144,8 @@ struct trpo_engine {
                       WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
       }
     };
-    // With two hidden layers under the tail and the fused layer-1 R-backward, the one weight-gradient GEMM left
-    // (layer 1: RH1, D1, H1 and the tail's RD1) does not depend on the R-backward: with option dual it runs on
-    // the side stream beside it (fork / join events; captured like the rest of the prefix)
-    if (g_options.dual != 0 && side && r0f && tail_fused && L == 3) {
-      HIPCHECK(hipEventRecord(ev_fork, stream));
-      HIPCHECK(hipStreamWaitEvent(side, ev_fork, 0));
-      std::swap(stream, side);
-      weight_grads();
-      std::swap(stream, side);
-      r_backward();
-      HIPCHECK(hipEventRecord(ev_join, side));
-      HIPCHECK(hipStreamWaitEvent(stream, ev_join, 0));
-    } else {
-      r_backward();
-      weight_grads();
-    }
+    r_backward();
+    weight_grads();
     reduce_grad(out, skip);
   }
 
@@ -1491,6 +1383,8 @@ struct trpo_engine {
     const void* host_ar;
     int rank, world;
     int cg_iters, adv, baseline;
+    int x_planes;   // X's planes hold the current batch: the captured plane kernels read them (set_batch
+                    // writes them outside the graph, so a replay must not outlive a change of this flag)
     float tol, damping;
     double gamma;
     Options opt;
@@ -1507,6 +1401,7 @@ struct trpo_engine {
     k.cg_iters = prm.cg_iters;
     k.adv = prm.compute_advantages != 0;
     k.baseline = have_baseline;
+    k.x_planes = x_planes ? 1 : 0;
     k.tol = prm.residual_tol;
     k.damping = prm.cg_damping;
     k.gamma = prm.compute_advantages ? prm.gamma : 0.0;
@@ -2404,11 +2299,6 @@ int trpo_discount(const double* x, const uint8_t* starts, int64_t n, double gamm
 }
 
 static int* option_slot(const std::string& k) {
-  if (k == "row_cfg") return &g_options.row_cfg;
-  if (k == "wg_cfg") return &g_options.wg_cfg;
-  if (k == "fused_head") return &g_options.fused_head;
-  if (k == "head_bwd") return &g_options.head_bwd;
-  if (k == "narrow_pf") return &g_options.narrow_pf;
   if (k == "split_mfma") return &g_options.split_mfma;
   if (k == "split_wg") return &g_options.split_wg;
   if (k == "chain") return &g_options.chain;
@@ -2419,9 +2309,7 @@ static int* option_slot(const std::string& k) {
   if (k == "fused") return &g_options.fused;
   if (k == "low_seg") return &g_options.low_seg;
   if (k == "planes") return &g_options.planes;
-  if (k == "e16") return &g_options.e16;
   if (k == "rbwd0") return &g_options.rbwd0;
-  if (k == "dual") return &g_options.dual;
   throw ArgError("unknown option " + k);
 }
 

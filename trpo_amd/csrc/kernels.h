@@ -13,13 +13,9 @@ namespace trpo {
 // Kernel-variant switches (defaults from TRPO_ROWCFG / TRPO_WGCFG / TRPO_FUSED_HEAD /
 // TRPO_HEAD_BWD; runtime-settable through trpo_set_option for A/B and parity tests).
 struct Options {
-  int row_cfg;     // wide row-GEMM tile: 0 = 128x256 (8 waves), 1 = 128x128, 2 = 256x128, 3 = BK32, 4 = 64x256, 5 = 256x256
-  int wg_cfg;      // 256x256 weight-gradient tile: 0 = BK16, 1 = BK32
-  int fused_head;  // engine: last-layer R-fwd + R-bwd + wgrad in one LDS-resident kernel
-  int head_bwd;    // engine: last-layer R-bwd + wgrad in one kernel
-  int narrow_pf;   // prefetch depth (1 or 2) of the memory-bound narrow tiles (softmax head, 128x256 wgrad)
-  int split_mfma;  // row GEMMs with N > 128 on bf16 MFMA with fp32 operands split 3 ways (hi+mid+lo)
-  int split_wg;    // weight gradients with fan_out > 128 on the split-bf16 MFMA (tile choice 1..3)
+  int split_mfma;  // row GEMMs with N > 128 on the split MFMA: 0 off (f32 MFMA), 5 = 256 x 256 tile
+                   // (default), any other value = 128 x 256
+  int split_wg;    // weight gradients with fan_out > 128 on the split MFMA: 0 off (f32 MFMA), 1 on
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
   int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
@@ -30,11 +26,8 @@ struct Options {
                    // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
   int planes;      // engine: row GEMMs whose operands have pre-split k-blocked f16 planes take the LDS-DMA
                    // plane kernel (plane.hip): 0 off, 1 on
-  int e16;         // engine: the tanh'' terms E_l read by per-layer R-backward row GEMMs are kept as 16-bit
-                   // high/low planes (RowEpi::kRBwd16): 0 off (f32), 1 on
   int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
-  int dual;        // engine: the FVP's weight-gradient GEMMs on a second stream beside the R-backward: 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -95,15 +88,7 @@ enum class RowEpi : int {
   kRZ = 11,       // RZ = acc + bias                             (R-forward pre-activation of the last
                   //                                              hidden layer: the fused tail applies
                   //                                              (1-H^2) as it loads H, so H is read once)
-  // E as two 16-bit planes (RowEpiArgs::e16_lo): the high and the low half of each f32 word, so a
-  // reader of both halves gets the f32 value bit for bit and a reader of the high half alone gets E
-  // truncated to 8 significant bits (the E RH term is O(eps) against the R-backward's main term)
-  kPrepBwd16 = 12,   // kPrepBwd with E (out1) as 16-bit planes
-  kPrepBwdE16 = 13,  // kPrepBwdE with E (out0) as 16-bit planes; running max |E| into amax0
-  kRBwd16 = 14,      // kRBwd with E as 16-bit planes; the low half is skipped when amaxE/amaxRH put the
-                     // E RH term >= low_seg + 3 binades below the main term's product scale
 };
-constexpr bool epi_e16(int e) { return e >= (int)RowEpi::kPrepBwd16 && e <= (int)RowEpi::kRBwd16; }
 // the row-wise softmax heads (one output row per 32-lane wave half, up to kMaxHeadTiles 32-column tiles)
 constexpr int kMaxHeadTiles = 4;
 constexpr bool epi_is_head(int e) { return e >= (int)RowEpi::kPrepHead && e <= (int)RowEpi::kRHead; }
@@ -129,11 +114,6 @@ struct RowEpiArgs {
   unsigned* amax0 = nullptr;
   unsigned* amax1 = nullptr;
   unsigned* amax2 = nullptr;
-  // 16-bit E planes (kPrepBwd16 / kPrepBwdE16 / kRBwd16): E's buffer holds the high halves at [0, .) and
-  // the low halves at e16_lo (uint16 elements) onward, both [M][ldo]
-  int64_t e16_lo = 0;
-  const unsigned* amaxE = nullptr;    // kRBwd16: running max |E| and |RH| (the high-half-only test)
-  const unsigned* amaxRH = nullptr;
 };
 
 struct RowGemmArgs {
@@ -324,59 +304,6 @@ void launch_adv_sq_partials(const double* adv, int64_t n, const double* global_s
 void launch_adv_normalize(double* adv, float* adv32, int64_t n, const double* global_sum,
                           const double* global_sq, double inv_n, hipStream_t s);
 
-}  // namespace trpo
-
-namespace trpo {
-// ---------------------------------------------------------------------------
-// Fused FVP head (gemm.hip): for the last layer (hidden width a <= 256, A <= 32)
-// one persistent kernel per split-K slab does, per 64-row tile held in LDS:
-//   RZ = RH W + H V + c ; RD_L = R-softmax-reverse(RZ)          (R-forward head)
-//   RD_{L-2} = (RD_L W^T + D_L V^T)(1-H^2) + E RH               (R-backward, hidden L-1)
-//   slab += RH^T D_L + H^T RD_L ; bias += colsum RD_L            (weight gradient, layer L-1)
-// ---------------------------------------------------------------------------
-struct HeadArgs {
-  int rows, a, b, apad, bpad;
-  const float* RH;   // [rows][apad]
-  const float* H;    // [rows][apad]
-  const float* WF;   // [2apad][bpad]  (W ; V)
-  const float* WB;   // [2bpad][apad]  (W^T ; V^T)
-  const float* c;    // [b] tangent bias
-  const float* P;    // [rows][bpad]
-  const float* DL;   // [rows][bpad]
-  const float* E;    // [rows][apad]
-  float* RDout;      // [rows][apad]
-  double invN;
-  int splits, rows_per_split;
-  float* slab;
-  int64_t slab_stride, off_w, off_b;
-  const int* skip;
-};
-void launch_fvp_head(const HeadArgs& a, hipStream_t s);
-}  // namespace trpo
-
-namespace trpo {
-// ---------------------------------------------------------------------------
-// Fused last-layer R-backward + weight gradient (gemm.hip), persistent per split:
-//   RD_{L-2} = ([RD_L | D_L] [W^T ; V^T]) (1 - H^2) + E RH       (hidden L-1, width a)
-//   slab    += RH^T D_L + H^T RD_L ;  bias += colsum RD_L          (layer L-1, a x b)
-// H / RH / E are read once, in MFMA accumulator layout, and reused as the A
-// operands of the weight-gradient MFMAs (rows as the K dimension).
-// ---------------------------------------------------------------------------
-struct HeadBwdArgs {
-  int rows, a, b, apad, bpad;
-  const float* RH;   // [rows][apad]
-  const float* H;    // [rows][apad]
-  const float* E;    // [rows][apad]
-  const float* WB;   // [2bpad][apad]  (W^T ; V^T)
-  const float* RDL;  // [rows][bpad]
-  const float* DL;   // [rows][bpad]
-  float* RDout;      // [rows][apad]
-  int splits, rows_per_split;
-  float* slab;
-  int64_t slab_stride, off_w, off_b;
-  const int* skip;
-};
-void launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {

@@ -244,9 +244,6 @@ void launch_rowgemm_planes(const RowGemmArgs& a, hipStream_t s) {
     case RowEpi::kTanh: launch_row_pl<(int)RowEpi::kTanh>(a, s); break;
     case RowEpi::kRHidden: launch_row_pl<(int)RowEpi::kRHidden>(a, s); break;
     case RowEpi::kRZ: launch_row_pl<(int)RowEpi::kRZ>(a, s); break;
-    case RowEpi::kPrepBwd16: launch_row_pl<(int)RowEpi::kPrepBwd16>(a, s); break;
-    case RowEpi::kPrepBwdE16: launch_row_pl<(int)RowEpi::kPrepBwdE16>(a, s); break;
-    case RowEpi::kRBwd16: launch_row_pl<(int)RowEpi::kRBwd16>(a, s); break;
     case RowEpi::kPrepBwd: launch_row_pl<(int)RowEpi::kPrepBwd>(a, s); break;
     case RowEpi::kPgBwd: launch_row_pl<(int)RowEpi::kPgBwd>(a, s); break;
     case RowEpi::kPrepBwdE: launch_row_pl<(int)RowEpi::kPrepBwdE>(a, s); break;

@@ -148,12 +148,6 @@ __device__ __forceinline__ void epi_elem(const RowEpiArgs& e, int row, int col, 
   }
 }
 
-// E from its 16-bit high / low planes (RowEpi::kRBwd16), bit for bit
-__device__ __forceinline__ float e16_load(const RowEpiArgs& e, size_t idx) {
-  const uint16_t* p = reinterpret_cast<const uint16_t*>(e.E);
-  return __builtin_bit_cast(float, ((unsigned)p[idx] << 16) | (unsigned)p[e.e16_lo + idx]);
-}
-
 // value part (loads + math) and store part of the element-wise epilogues.
 // No column predicate: padding columns (col >= N) have zero accumulators (zero
 // weight padding), zero bias and zero H/E/RH padding, so every formula below
@@ -168,14 +162,12 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
     o0 = one_minus_sq(e.H[idx]) * (v + bv);
   } else if constexpr (EPI == (int)RowEpi::kRZ) {
     o0 = v + bv;
-  } else if constexpr (EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16) {
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwd) {
     const float h = e.H[idx];
     o0 = v * one_minus_sq(h);
     o1 = -2.0f * v * h;
-  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPrepBwdE16) {
+  } else if constexpr (EPI == (int)RowEpi::kPrepBwdE) {
     o0 = -2.0f * v * e.H[idx];
-  } else if constexpr (EPI == (int)RowEpi::kRBwd16) {
-    o0 = fmaf(e16_load(e, idx), e.RH[idx], v * one_minus_sq(e.H[idx]));
   } else if constexpr (EPI == (int)RowEpi::kPgBwd) {
     o0 = v * one_minus_sq(e.H[idx]);
   } else if constexpr (EPI == (int)RowEpi::kRBwd) {
@@ -188,19 +180,8 @@ __device__ __forceinline__ void epi_elem_v(const RowEpiArgs& e, size_t idx, bool
 }
 template <int EPI>
 __device__ __forceinline__ void epi_store(const RowEpiArgs& e, size_t idx, float o0, float o1) {
-  auto st16 = [&](float* base, float v) {   // the two 16-bit halves of v into E's planes
-    uint16_t* p = reinterpret_cast<uint16_t*>(base);
-    const unsigned b = __builtin_bit_cast(unsigned, v);
-    p[idx] = (uint16_t)(b >> 16);
-    p[e.e16_lo + idx] = (uint16_t)(b & 0xffffu);
-  };
-  if constexpr (EPI == (int)RowEpi::kPrepBwdE16) {
-    st16(e.out0, o0);
-  } else {
-    e.out0[idx] = o0;
-    if constexpr (EPI == (int)RowEpi::kPrepBwd) e.out1[idx] = o1;
-    if constexpr (EPI == (int)RowEpi::kPrepBwd16) st16(e.out1, o1);
-  }
+  e.out0[idx] = o0;
+  if constexpr (EPI == (int)RowEpi::kPrepBwd) e.out1[idx] = o1;
 }
 
 
@@ -370,8 +351,8 @@ __device__ __forceinline__ void tile_of(int ntn, int& mt, int& nt) {
 // descriptor (base = row m0, num_records = the rows this tile owns), so a load/store is one buffer op with
 // a lane-constant voffset and a per-row SGPR soffset; rows past M fall outside the descriptor (loads read
 // 0, stores are dropped) -- no per-element predicate, no 64-bit address math, and all 16 loads of a chunk
-// stay in flight.  ETRUNC (kRBwd16 only): read the high halves of E alone.
-template <int WM, int WN, int TM, int TN, int EPI, bool ETRUNC>
+// stay in flight.
+template <int WM, int WN, int TM, int TN, int EPI>
 __device__ __forceinline__ void row_epi_full(const RowGemmArgs& args, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
                                              int wn, int lr, int lh, float& mx0, float& mx1) {
   constexpr int BM = WM * TM * 32;
@@ -383,47 +364,24 @@ __device__ __forceinline__ void row_epi_full(const RowGemmArgs& args, f32x16 (&a
   auto mk = [&](const float* ptr) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(ptr + (size_t)m0 * ldo), 0, tile_bytes, 0x00020000);
   };
-  // E's 16-bit planes: the high halves from the buffer's base, the low halves e16_lo elements on
-  auto mk16 = [&](const float* ptr, bool lo) {
-    const uint16_t* p = reinterpret_cast<const uint16_t*>(ptr) + (lo ? e.e16_lo : 0) + (size_t)m0 * ldo;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, tile_bytes / 2, 0x00020000);
-  };
   constexpr bool kUsesH = EPI == (int)RowEpi::kRHidden || EPI == (int)RowEpi::kPrepBwd ||
                           EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPgBwd ||
-                          EPI == (int)RowEpi::kRBwd || EPI == (int)RowEpi::kReluBwd || epi_e16(EPI);
-  constexpr bool kRB16 = EPI == (int)RowEpi::kRBwd16;
-  constexpr bool kRB = EPI == (int)RowEpi::kRBwd || kRB16;
-  constexpr bool kTwo = EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16;
-  constexpr bool kPB = EPI == (int)RowEpi::kPrepBwd || EPI == (int)RowEpi::kPrepBwd16;
-  constexpr bool kPE = EPI == (int)RowEpi::kPrepBwdE || EPI == (int)RowEpi::kPrepBwdE16;
-  // where E goes as 16-bit planes: out1 (kPrepBwd16) or out0 (kPrepBwdE16)
-  constexpr int kE16Out = EPI == (int)RowEpi::kPrepBwd16 ? 1 : (EPI == (int)RowEpi::kPrepBwdE16 ? 0 : -1);
+                          EPI == (int)RowEpi::kRBwd || EPI == (int)RowEpi::kReluBwd;
+  constexpr bool kRB = EPI == (int)RowEpi::kRBwd;
+  constexpr bool kPB = EPI == (int)RowEpi::kPrepBwd;
+  constexpr bool kPE = EPI == (int)RowEpi::kPrepBwdE;
   // descriptors of operands an epilogue does not use alias out0 and are never touched
   const __amdgpu_buffer_rsrc_t rO0 = mk(e.out0);
   const __amdgpu_buffer_rsrc_t rH = mk(kUsesH ? e.H : e.out0);
-  const __amdgpu_buffer_rsrc_t rE = mk((kRB && !kRB16) ? e.E : e.out0);
-  const __amdgpu_buffer_rsrc_t rEh = mk16(kRB16 ? e.E : e.out0, false);
-  const __amdgpu_buffer_rsrc_t rEl = mk16(kRB16 ? e.E : e.out0, kRB16);
+  const __amdgpu_buffer_rsrc_t rE = mk(kRB ? e.E : e.out0);
   const __amdgpu_buffer_rsrc_t rRH = mk(kRB ? e.RH : e.out0);
-  const __amdgpu_buffer_rsrc_t rO1 = mk(kTwo ? e.out1 : e.out0);
-  const float* e16o = kE16Out == 1 ? e.out1 : e.out0;
-  const __amdgpu_buffer_rsrc_t rSh = mk16(e16o, false);
-  const __amdgpu_buffer_rsrc_t rSl = mk16(e16o, kE16Out >= 0);
+  const __amdgpu_buffer_rsrc_t rO1 = mk(kPB ? e.out1 : e.out0);
   const int vbase = ((wm * TM * 32 + 4 * lh) * ldo + n0 + wn * TN * 32 + lr) * 4;
   auto ld = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
   };
-  auto ld16 = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) {
-    return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, vo >> 1, so >> 1, 0);
-  };
   auto st = [&](float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
-  };
-  auto st16 = [&](float v, int vo, int so) {
-    const unsigned b = __builtin_bit_cast(unsigned, v);
-    // (the b16 buffer builtins take and return unsigned short: raw bits, no conversion)
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b >> 16), rSh, vo >> 1, so >> 1, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b & 0xffffu), rSl, vo >> 1, so >> 1, 0);
   };
   // Operand loads run one (tm, tn) chunk ahead of the chunk being computed and stored: the
   // chunk's loads are issued before the previous chunk's stores in program order (hipcc cannot
@@ -441,12 +399,7 @@ __device__ __forceinline__ void row_epi_full(const RowGemmArgs& args, f32x16 (&a
         const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
         dst[0][r] = ld(rH, vo, so);
         if constexpr (NL == 3) {
-          if constexpr (kRB16) {
-            const unsigned hi = ld16(rEh, vo, so) << 16;
-            dst[1][r] = __builtin_bit_cast(float, ETRUNC ? hi : (hi | ld16(rEl, vo, so)));
-          } else {
-            dst[1][r] = ld(rE, vo, so);
-          }
+          dst[1][r] = ld(rE, vo, so);
           dst[2][r] = ld(rRH, vo, so);
         }
       }
@@ -505,27 +458,11 @@ __device__ __forceinline__ void row_epi_full(const RowGemmArgs& args, f32x16 (&a
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int so = (tm * 32 + (r & 3) + 8 * (r >> 2)) * ldo * 4;
-        if constexpr (kE16Out == 0) st16(o0[r], vo, so);
-        else st(o0[r], rO0, vo, so);
-        if constexpr (EPI == (int)RowEpi::kPrepBwd) st(o1[r], rO1, vo, so);
-        if constexpr (kE16Out == 1) st16(o1[r], vo, so);
+        st(o0[r], rO0, vo, so);
+        if constexpr (kPB) st(o1[r], rO1, vo, so);
       }
     }
   }
-}
-
-__device__ __forceinline__ int amax_exp(const unsigned* amax);
-
-// kRBwd16: whether E's high halves alone are enough -- the E RH term's running-max product scale sits at
-// least low_seg + 3 binades below the main term's (segment 0, RD W^T): truncation to 8 significant bits
-// (2^-7 relative) then stays 2^-(low_seg - 4) below the dominant products, the one-product segment's bar
-// (rowgemm3_kernel).  Uniform over the launch.
-__device__ __forceinline__ bool e16_trunc_ok(const RowGemmArgs& args) {
-  const RowEpiArgs& e = args.ea;
-  if (args.low_seg <= 0 || !e.amaxE || !e.amaxRH || !args.seg[0].amaxA || !args.seg[0].amaxB) return false;
-  const int qE = amax_exp(e.amaxE) + amax_exp(e.amaxRH);
-  const int q0 = amax_exp(args.seg[0].amaxA) + amax_exp(args.seg[0].amaxB);
-  return __builtin_amdgcn_readfirstlane(qE - q0 >= args.low_seg + 3 ? 1 : 0) != 0;
 }
 
 // Fused epilogue of a row-GEMM tile.  The accumulator layout (col = lane&31,
@@ -553,12 +490,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& args, f32x16 (&a
   } else {
     const bool fulln = (n0 + BN <= args.Npad);
     if (fulln) {
-      if constexpr (EPI == (int)RowEpi::kRBwd16) {
-        if (e16_trunc_ok(args)) row_epi_full<WM, WN, TM, TN, EPI, true>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
-        else row_epi_full<WM, WN, TM, TN, EPI, false>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
-      } else {
-        row_epi_full<WM, WN, TM, TN, EPI, false>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
-      }
+      row_epi_full<WM, WN, TM, TN, EPI>(args, acc, m0, n0, wm, wn, lr, lh, mx0, mx1);
     } else {
       // partial-width tile (odd layer widths): predicated path
 #pragma unroll
