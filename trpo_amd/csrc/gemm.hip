@@ -193,11 +193,16 @@ rowgemm_kernel(const RowGemmArgs args) {
 
 
 
-template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF, int NP>
+template <int WM, int WN, int TM, int TN, int EPI, int OCC, int PF, int NP, int BKT = 16>
 __global__ void __launch_bounds__(WM* WN * 64, OCC)   // OCC waves / SIMD
 rowgemm3_kernel(const RowGemmArgs args) {
   // NP = 3: bf16 hi/mid/lo planes, 6 products ; NP = 2: scaled f16 hi/lo planes, 3 products
-  constexpr int BK = 16;
+  // BKT = 16: 32-B LDS rows (swz16) ; 32: 64-B rows, chunks XOR-swizzled by row bits 2-3 (plane.hip's pl_swz), two
+  // MFMA k-steps per staged tile and half the barriers (B planes' ldk a multiple of 32: launch_row3_cfg)
+  constexpr int BK = BKT;
+  static_assert(BK == 16 || BK == 32, "rowgemm3 k-tile");
+  auto swk = [](int r, int c) { return BK == 16 ? swz16(r, c) : r * 32 + ((c ^ ((r >> 2) & 3)) << 3); };
+  constexpr int CB = BK / 8;   // 16-B chunks per row of a staged tile
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int APL = BM * BK, BPL = BN * BK;     // one plane
   constexpr int STG = NP * (APL + BPL);
@@ -249,7 +254,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   constexpr int AF4 = BM * BK / 4;          // f32x4 of A per k-tile
-  constexpr int BC = NP * BN * (BK / 8);    // 16-B chunks of B planes per k-tile
+  constexpr int BC = NP * BN * CB;          // 16-B chunks of B planes per k-tile
   constexpr int AP = (AF4 + NT - 1) / NT, BP = (BC + NT - 1) / NT;
   // Staging loads are buffer ops on per-segment descriptors (rows [m0, M) of A; the B planes): rows past
   // M and k past the segment's K read 0 and invalid B columns address past the end, so a load is one
@@ -268,8 +273,8 @@ rowgemm3_kernel(const RowGemmArgs args) {
 #pragma unroll
   for (int i = 0; i < BP; ++i) {
     const int f = tid + i * NT;
-    const int p = f / (BN * 2), rem = f % (BN * 2);
-    const int n = rem >> 1, kh = rem & 1;
+    const int p = f / (BN * CB), rem = f % (BN * CB);
+    const int n = rem / CB, kh = rem % CB;
     const bool ok = (BC % NT == 0 || f < BC) && n0 + n < args.Npad;
     vBo[i] = ok ? (p * planeB + (n0 + n) * ldkB + 8 * kh) * 2 : kOob;
   }
@@ -309,7 +314,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
       if (AF4 % NT == 0 || f < AF4) {
         const int r = f / (BK / 4), kq = f % (BK / 4);
         const f32x4 x = st.ra[i];
-        unsigned short* dst = As + swz16(r, kq >> 1) + 4 * (kq & 1);
+        unsigned short* dst = As + swk(r, kq >> 1) + 4 * (kq & 1);
         if constexpr (NP == 3) {
           u16x4 h, m, l;
 #pragma unroll
@@ -342,9 +347,9 @@ rowgemm3_kernel(const RowGemmArgs args) {
     for (int i = 0; i < BP; ++i) {
       const int f = tid + i * NT;
       if (BC % NT == 0 || f < BC) {
-        const int p = f / (BN * 2), rem = f % (BN * 2);
-        const int n = rem >> 1, kh = rem & 1;
-        *reinterpret_cast<u16x8*>(Bs + p * BPL + swz16(n, kh)) = st.rb[i];
+        const int p = f / (BN * CB), rem = f % (BN * CB);
+        const int n = rem / CB, kh = rem % CB;
+        *reinterpret_cast<u16x8*>(Bs + p * BPL + swk(n, kh)) = st.rb[i];
       }
     }
   };
@@ -354,13 +359,15 @@ rowgemm3_kernel(const RowGemmArgs args) {
     const unsigned short* Bs = As + NP * APL;
     // fragments streamed per output column tile to keep few registers live
 #pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const int bo = swz16(wn * TN * 32 + tn * 32 + lr, lh);
+      const int bo = swk(wn * TN * 32 + tn * 32 + lr, 2 * ks + lh);
       if constexpr (NP == 2 && ONE) {
         const f16x8 b0 = *reinterpret_cast<const f16x8*>(Bs + bo);
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
-          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+          const int ao = swk(wm * TM * 32 + tm * 32 + lr, 2 * ks + lh);
           const f16x8 a0 = *reinterpret_cast<const f16x8*>(As + ao);
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[tm][tn], 0, 0, 0);
         }
@@ -371,7 +378,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
           bf16x8 a[3];
-          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+          const int ao = swk(wm * TM * 32 + tm * 32 + lr, 2 * ks + lh);
 #pragma unroll
           for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(As + p * APL + ao);
           // smallest terms first
@@ -391,7 +398,7 @@ rowgemm3_kernel(const RowGemmArgs args) {
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
           f16x8 a[2];
-          const int ao = swz16(wm * TM * 32 + tm * 32 + lr, lh);
+          const int ao = swk(wm * TM * 32 + tm * 32 + lr, 2 * ks + lh);
 #pragma unroll
           for (int p = 0; p < 2; ++p) a[p] = *reinterpret_cast<const f16x8*>(As + p * APL + ao);
           f32x16 c = acc[tm][tn];
@@ -977,7 +984,7 @@ void launch_row_cfg(const RowGemmArgs& a, hipStream_t s) {
                      0, s, a);
 }
 
-template <int WM, int WN, int TM, int TN, int EPI, int OCC = 2, int PF = 1>
+template <int WM, int WN, int TM, int TN, int EPI, int OCC = 2, int PF = 1, int BKT = 16>
 void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   for (int i = 0; i < a.nseg; ++i)
@@ -990,12 +997,18 @@ void launch_row3_cfg(const RowGemmArgs& a, hipStream_t s) {
   const long nblk = (long)((a.M + BM - 1) / BM) * ((a.Npad + BN - 1) / BN);
   RowGemmArgs b = a;
   b.low_seg = g_options.low_seg;
+  if constexpr (BKT == 32) {
+    for (int i = 0; i < a.nseg; ++i)
+      if (a.seg[i].ldk % 32) throw std::runtime_error("split row GEMM (BK 32): B planes' ldk not a multiple of 32");
+  }
   if (a.f16)
-    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 2>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
-                       s, b);
+    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 2, BKT>), dim3((unsigned)nblk),
+                       dim3(WM * WN * 64), 0, s, b);
+  else if constexpr (BKT == 16)   // three bf16 planes at BK 32 exceed the LDS
+    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 3, BKT>), dim3((unsigned)nblk),
+                       dim3(WM * WN * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((rowgemm3_kernel<WM, WN, TM, TN, EPI, OCC, PF, 3>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
-                       s, a);
+    throw std::runtime_error("split row GEMM (BK 32): f16 planes only");
 }
 
 // A row GEMM whose k-loop is a few MFMA steps (the R-backward out of the softmax head: K = 2 x actions)
@@ -1017,9 +1030,18 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
     else if (a.N > 32) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
   } else if (rowgemm_uses_split(a.Npad, a.epi) && !small_k_row(a)) {
-    // split_mfma 5 (default): 256 x 256, two k-tiles in flight; any other non-zero value: 128 x 256
-    if (g_options.split_mfma == 5) launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
-    else launch_row3_cfg<2, 4, 2, 2, EPI>(a, s);
+    // split_mfma 5 (default): 256 x 256, two k-tiles in flight; 14: the same tile at BK 32 with one k-tile in
+    // flight; any other non-zero value: 128 x 256
+    if (g_options.split_mfma == 5) {
+      launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
+    } else if (g_options.split_mfma == 14) {   // 256 x 256 at BK 32, one k-tile in flight (f16 planes only)
+      bool ok = a.f16 != 0;
+      for (int i = 0; i < a.nseg; ++i) ok = ok && a.seg[i].ldk % 32 == 0;
+      if (ok) launch_row3_cfg<4, 2, 2, 4, EPI, 2, 1, 32>(a, s);
+      else launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
+    } else {
+      launch_row3_cfg<2, 4, 2, 2, EPI>(a, s);
+    }
   } else {
     if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
     else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
