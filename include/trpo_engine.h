@@ -189,7 +189,7 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
 
 /* ---- kernel-variant switches (for A/B measurements and variant parity tests) ----------
  * "split_mfma" (0 = f32 MFMA row GEMMs; 5 = the 256 x 256 split row-GEMM tile for outputs wider than
- * 128, the default; any other value = the 128 x 256 tile), "split_wg" (0 = f32 weight gradients;
+ * 128, at BK 32 on f16 planes, the default; 6 = the same tile at BK 16; any other value = 128 x 256), "split_wg" (0 = f32 weight gradients;
  * 1 = split tile for fan_out > 128), "chain" (fused FVP chain: 0 off, 1 auto, 2..4 forced variants),
  * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
  * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph, all-reduces

@@ -271,7 +271,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"chain": 2}, {"chain": 3},               # fused FVP chain forms (default 1 = auto)
     {"chain": 0},                               # per-layer row-GEMM FVP
     {"split_mfma": 0}, {"chain": 0, "split_mfma": 1}, {"chain": 0, "split_mfma": 5},
-    {"split_mfma": 14}, {"chain": 0, "split_mfma": 14},       # 256 x 256 at BK 32
+    {"split_mfma": 6}, {"chain": 0, "split_mfma": 6},         # 256 x 256 at BK 16 (round-3 default)
     {"split_wg": 0}, {"split_wg": 1},
     {"split_mfma": 5, "split_wg": 1},
     {"split_f16": 0}, {"split_f16": 0, "split_wg": 1},        # bf16 three-piece split (6 products)

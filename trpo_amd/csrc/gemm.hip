@@ -1030,18 +1030,14 @@ void launch_row_epi(const RowGemmArgs& a, hipStream_t s) {
     else if (a.N > 32) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);
     else launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
   } else if (rowgemm_uses_split(a.Npad, a.epi) && !small_k_row(a)) {
-    // split_mfma 5 (default): 256 x 256, two k-tiles in flight; 14: the same tile at BK 32 with one k-tile in
-    // flight; any other non-zero value: 128 x 256
-    if (g_options.split_mfma == 5) {
-      launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
-    } else if (g_options.split_mfma == 14) {   // 256 x 256 at BK 32, one k-tile in flight (f16 planes only)
-      bool ok = a.f16 != 0;
-      for (int i = 0; i < a.nseg; ++i) ok = ok && a.seg[i].ldk % 32 == 0;
-      if (ok) launch_row3_cfg<4, 2, 2, 4, EPI, 2, 1, 32>(a, s);
-      else launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
-    } else {
-      launch_row3_cfg<2, 4, 2, 2, EPI>(a, s);
-    }
+    // split_mfma 5 (default): 256 x 256 tile, BK 32 with one k-tile in flight on f16 planes whose ldk is a
+    // multiple of 32 (C4 A/B, profiles/r4b: 2.260 -> 2.281 updates/s), else BK 16 with two in flight;
+    // 6: 256 x 256 at BK 16 always (the round-3 default); any other non-zero value: 128 x 256
+    bool bk32 = a.f16 != 0 && g_options.split_mfma == 5;
+    for (int i = 0; i < a.nseg; ++i) bk32 = bk32 && a.seg[i].ldk % 32 == 0;
+    if (bk32) launch_row3_cfg<4, 2, 2, 4, EPI, 2, 1, 32>(a, s);
+    else if (g_options.split_mfma == 5 || g_options.split_mfma == 6) launch_row3_cfg<4, 2, 2, 4, EPI, 2, 2>(a, s);
+    else launch_row3_cfg<2, 4, 2, 2, EPI>(a, s);
   } else {
     if (a.Npad <= 32) launch_row_cfg<4, 1, 2, 1, 16, EPI>(a, s);
     else if (a.Npad <= 64) launch_row_cfg<4, 1, 2, 2, 16, EPI>(a, s);

@@ -13,8 +13,8 @@ namespace trpo {
 // Kernel-variant switches (defaults from TRPO_ROWCFG / TRPO_WGCFG / TRPO_FUSED_HEAD /
 // TRPO_HEAD_BWD; runtime-settable through trpo_set_option for A/B and parity tests).
 struct Options {
-  int split_mfma;  // row GEMMs with N > 128 on the split MFMA: 0 off (f32 MFMA), 5 = 256 x 256 tile
-                   // (default), any other value = 128 x 256
+  int split_mfma;  // row GEMMs with N > 128 on the split MFMA: 0 off (f32 MFMA), 5 = 256 x 256 tile at
+                   // BK 32 on f16 planes (default), 6 = 256 x 256 at BK 16, any other value = 128 x 256
   int split_wg;    // weight gradients with fan_out > 128 on the split MFMA: 0 off (f32 MFMA), 1 on
   int chain;       // FVP R-forward + R-backward as one fused kernel (chain.hip): 0 off, 1 auto, 2..4 variant
   int split_f16;   // split GEMMs on f16 MFMA: operands scaled by powers of two and split hi+lo (3 products)
