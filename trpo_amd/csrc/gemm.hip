@@ -37,7 +37,7 @@ static int env_int(const char* name, int dflt) {
 Options g_options = {env_int("TRPO_SPLIT_MFMA", 5), env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1),
                      env_int("TRPO_SPLIT_F16", 1), env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1),
                      env_int("TRPO_TAIL", 1), env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14),
-                     env_int("TRPO_PLANES", 1), env_int("TRPO_RBWD0", 1)};
+                     env_int("TRPO_PLANES", 1), env_int("TRPO_RBWD0", 1), env_int("TRPO_RD_PLANES", 1)};
 
 namespace {
 
@@ -555,6 +555,22 @@ wgrad3_kernel(const WGradArgs args) {
   auto ldbuf = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
   };
+  // segments whose B is a per-tile-scaled plane pair (WSeg::Bh): lane offsets into the planes of this split's
+  // rows (k-block of the lane's column, its 8-row group)
+  int vBp[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int f = tid + i * NT;
+    const int c = f % BN, g = f / BN;
+    const bool okc = (BI % NT == 0 || f < BI) && n0 + c < args.Npad;
+    const int col = n0 + c;
+    // offsets reach 3.6 GB at C4 (past int32): unsigned bits, with an all-ones out-of-range sentinel
+    vBp[i] = (int)(okc ? (unsigned)((((int64_t)(col >> 5) * args.seg[1].b_mpad + 8 * g) * 32 + (col & 31)) * 2)
+                       : 0xFFFFFFF0u);
+  }
+  auto ld16f = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0));
+  };
   struct Stage {
     float va[AP][8], vb[BP][8];
     bool cs;         // this tile belongs to the column-summed segment
@@ -575,10 +591,33 @@ wgrad3_kernel(const WGradArgs args) {
     for (int i = 0; i < AP; ++i)
 #pragma unroll
       for (int q = 0; q < 8; ++q) st.va[i][q] = ldbuf(ra, vA[i], sa + q * lda4);
+    const WSeg& sgw = sg ? args.seg[1] : args.seg[0];
+    if (NP == 2 && sgw.Bh) {
+      // (hi + lo) 2^-e of the k-tile's 32-row tile (k-tiles of 16 rows never straddle one: r0 % 32 == 0);
+      // rows past the split (another split's, or past the shard) are zeroed
+      const int e = sgw.eBt[(r0 + kt * BK) >> 5];
+      const float inv = __builtin_ldexpf(1.0f, -e);
+      const unsigned nbytes = (unsigned)((((int64_t)(args.Npad - 1) >> 5) * sgw.b_mpad + (r1 - r0)) * 64);
+      const __amdgpu_buffer_rsrc_t rh =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bh + (size_t)r0 * 32), 0, nbytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rl =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bl + (size_t)r0 * 32), 0, nbytes, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < BP; ++i)
+      for (int i = 0; i < BP; ++i) {
+        const int gq = (tid + i * NT) / BN;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) st.vb[i][q] = ldbuf(rb, vB[i], sb + q * ldb4);
+        for (int q = 0; q < 8; ++q) {
+          const int so = (kt * BK + q) * 64;
+          const float v = (ld16f(rh, vBp[i], so) + ld16f(rl, vBp[i], so)) * inv;
+          st.vb[i][q] = r0 + kt * BK + 8 * gq + q < r1 ? v : 0.0f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BP; ++i)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st.vb[i][q] = ldbuf(rb, vB[i], sb + q * ldb4);
+    }
     __builtin_amdgcn_sched_barrier(0);
   };
   auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int e) {
@@ -1061,6 +1100,13 @@ void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
     throw std::runtime_error("split-bf16 wgrad: segments with different leading dimensions");
   if ((int64_t)a.rows_per_split * (a.seg[0].lda > a.seg[0].ldb ? a.seg[0].lda : a.seg[0].ldb) * 4 >= (int64_t(1) << 30))
     throw std::runtime_error("split-bf16 wgrad: a split's rows exceed the 1 GiB buffer-descriptor range");
+  for (int i = 0; i < a.nseg; ++i) {
+    const WSeg& sg = a.seg[i];
+    if (!sg.Bh) continue;
+    if (!a.f16 || i != 1 || !sg.Bl || !sg.eBt || a.rows_per_split % 32 || sg.b_mpad < a.rows ||
+        (((int64_t)(a.Npad - 1) >> 5) * sg.b_mpad + a.rows_per_split) * 64 >= (int64_t(1) << 32) - 64)
+      throw std::runtime_error("split wgrad: B planes need f16, segment 1, 32-row splits and a 4 GiB range");
+  }
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
   WGradArgs b = a;
   b.low_seg = g_options.low_seg;
