@@ -145,7 +145,7 @@ struct trpo_engine {
   int rd_mpad = 0;
   bool use_rd_planes() const {
     return RDh && g_options.rd_planes != 0 && L == 3 && use_tail() && use_rbwd0() && d1_plane && d1_lo &&
-           !use_fused() &&
+           !use_fused() && g_options.split_wg != 0 && w[2] > 128 &&   // layer 1's wgrad on the split tile (gemm.hip)
            !use_chain() && wp[2] % 64 == 0 && r16(wp[2]) % 32 == 0;
   }
   uint16_t* tail_planes = nullptr;   // head planes of the fused FVP tail (tail.hip), [2][2][32][kTailK]

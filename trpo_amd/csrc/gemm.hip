@@ -1161,6 +1161,8 @@ void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
 void launch_wgrad(const WGradArgs& a, hipStream_t s) {
   if (a.splits <= 0) return;
   const int Mp = a.Ma, Np = a.Nb;
+  if ((a.seg[0].Bh || (a.nseg > 1 && a.seg[1].Bh)) && !(Np > 128 && g_options.split_wg != 0))
+    throw std::runtime_error("wgrad: B planes are read by the split weight-gradient tile only");
   // output tile by (fan_in, fan_out); every B column set of one split lives in one block row
   if (Np <= 32) {
     if (Mp <= 64) launch_wg_cfg<2, 1, 1, 1>(a, s);          // 64 x 32
