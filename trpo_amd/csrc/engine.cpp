@@ -408,7 +408,7 @@ struct trpo_engine {
       RDh = dalloc<uint16_t>((size_t)rd_mpad * wp[2]);
       RDl = dalloc<uint16_t>((size_t)rd_mpad * wp[2]);
       D1l = dalloc<uint16_t>((size_t)((cap + 255) / 256 * 256) * d1_ldp);
-      eRD = dalloc<int>((size_t)rd_mpad / 32 + 8);
+      eRD = dalloc<int>(((size_t)rd_mpad / 32 + 8) * (wp[2] / 32));   // one per 32 x 32 block
       W1Tb = dalloc<uint16_t>(2 * plane3_b(1));
       V1Tb = dalloc<uint16_t>(2 * plane3_b(1));
     }

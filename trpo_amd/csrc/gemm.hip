@@ -555,27 +555,23 @@ wgrad3_kernel(const WGradArgs args) {
   auto ldbuf = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
   };
-  // segments whose B is a per-tile-scaled plane pair (WSeg::Bh): lane offsets into the planes of this split's
-  // rows (k-block of the lane's column, its 8-row group)
-  int vBp[BP];
-#pragma unroll
-  for (int i = 0; i < BP; ++i) {
-    const int f = tid + i * NT;
-    const int c = f % BN, g = f / BN;
-    const bool okc = (BI % NT == 0 || f < BI) && n0 + c < args.Npad;
-    const int col = n0 + c;
-    // offsets reach 3.6 GB at C4 (past int32): unsigned bits, with an all-ones out-of-range sentinel
-    vBp[i] = (int)(okc ? (unsigned)((((int64_t)(col >> 5) * args.seg[1].b_mpad + 8 * g) * 32 + (col & 31)) * 2)
-                       : 0xFFFFFFF0u);
-  }
-  auto ld16f = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
-    return (float)__builtin_bit_cast(_Float16, __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0));
-  };
+  // segments whose B is a plane pair with per-block scales (WSeg::Bh): thread tid < BN loads columns 2p, 2p + 1
+  // (p = tid % (BN / 2)) of 8-row group tid / (BN / 2), one 4-byte load per plane and row
+  const int pp = tid % (BN / 2), pg = tid / (BN / 2);
+  const int pcol = n0 + 2 * pp;
+  const bool pok = pcol < args.Npad;
+  // offsets reach 3.6 GB at C4 (past int32): unsigned bits, with an all-ones out-of-range sentinel
+  const int vBp = (int)(pok ? (unsigned)((((int64_t)(pcol >> 5) * args.seg[1].b_mpad + 8 * pg) * 32 + (pcol & 31)) * 2)
+                            : 0xFFFFFFF0u);
+
   struct Stage {
     float va[AP][8], vb[BP][8];
+    float vp[2][8];  // a plane segment (WSeg::Bh): threads tid < BN hold columns 2p, 2p + 1 of their 8 rows
     bool cs;         // this tile belongs to the column-summed segment
     int sg;          // segment
+    bool pl;         // the tile's B comes from planes
   };
+  float csp[2] = {0.0f, 0.0f};   // plane segments' column sums (columns 2p, 2p + 1)
   auto gload = [&](Stage& st, int t) {
     const int sg = t / nk;
     const int kt = t - sg * nk;
@@ -592,24 +588,28 @@ wgrad3_kernel(const WGradArgs args) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) st.va[i][q] = ldbuf(ra, vA[i], sa + q * lda4);
     const WSeg& sgw = sg ? args.seg[1] : args.seg[0];
+    st.pl = NP == 2 && sgw.Bh != nullptr;
     if (NP == 2 && sgw.Bh) {
-      // (hi + lo) 2^-e of the k-tile's 32-row tile (k-tiles of 16 rows never straddle one: r0 % 32 == 0);
-      // rows past the split (another split's, or past the shard) are zeroed
-      const int e = sgw.eBt[(r0 + kt * BK) >> 5];
-      const float inv = __builtin_ldexpf(1.0f, -e);
-      const unsigned nbytes = (unsigned)((((int64_t)(args.Npad - 1) >> 5) * sgw.b_mpad + (r1 - r0)) * 64);
-      const __amdgpu_buffer_rsrc_t rh =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bh + (size_t)r0 * 32), 0, nbytes, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rl =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bl + (size_t)r0 * 32), 0, nbytes, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < BP; ++i) {
-        const int gq = (tid + i * NT) / BN;
+      // (hi + lo) 2^-e of the lane's 32 x 32 block (k-tiles of 16 rows never straddle a block row:
+      // r0 % 32 == 0); rows past the split (another split's, or past the shard) are zeroed
+      if (tid < BN) {
+        const int nkbB = args.Npad >> 5;
+        const int e = pok ? sgw.eBt[((r0 + kt * BK) >> 5) * nkbB + (pcol >> 5)] : 0;
+        const float inv = __builtin_ldexpf(1.0f, -e);
+        const unsigned nbytes = (unsigned)((((int64_t)(args.Npad - 1) >> 5) * sgw.b_mpad + (r1 - r0)) * 64);
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bh + (size_t)r0 * 32), 0, nbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bl + (size_t)r0 * 32), 0, nbytes, 0x00020000);
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int so = (kt * BK + q) * 64;
-          const float v = (ld16f(rh, vBp[i], so) + ld16f(rl, vBp[i], so)) * inv;
-          st.vb[i][q] = r0 + kt * BK + 8 * gq + q < r1 ? v : 0.0f;
+          const h2 hv = __builtin_bit_cast(h2, __builtin_amdgcn_raw_buffer_load_b32(rh, vBp, so, 0));
+          const h2 lv = __builtin_bit_cast(h2, __builtin_amdgcn_raw_buffer_load_b32(rl, vBp, so, 0));
+          const bool ok = r0 + kt * BK + 8 * pg + q < r1;
+          st.vp[0][q] = ok ? ((float)hv[0] + (float)lv[0]) * inv : 0.0f;
+          st.vp[1][q] = ok ? ((float)hv[1] + (float)lv[1]) * inv : 0.0f;
         }
       }
     } else {
@@ -656,6 +656,21 @@ wgrad3_kernel(const WGradArgs args) {
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
       if (AI % NT == 0 || f < AI) put(As, APL, f % BM, f / BM, st.va[i], eA[st.sg]);
+    }
+    if (NP == 2 && st.pl) {
+      if (tid < BN) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          put(Bs, BPL, 2 * pp + j, pg, st.vp[j], eB[st.sg]);
+          if (st.cs) {
+            float cs = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cs += st.vp[j][q];
+            csp[j] += cs;
+          }
+        }
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
@@ -795,10 +810,18 @@ wgrad3_kernel(const WGradArgs args) {
     }
   if (do_colsum) {
     // column sums: the two 8-row groups of a column, combined in a fixed order
+    const bool cs_planes = NP == 2 && args.seg[args.colsum_seg].Bh != nullptr;
+    if (cs_planes) {
+      if (tid < BN) {
+        cs_sh[pg][2 * pp] = csp[0];
+        cs_sh[pg][2 * pp + 1] = csp[1];
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < BP; ++i) {
-      const int f = tid + i * NT;
-      if (BI % NT == 0 || f < BI) cs_sh[f / BN][f % BN] = csum[i];
+      for (int i = 0; i < BP; ++i) {
+        const int f = tid + i * NT;
+        if (BI % NT == 0 || f < BI) cs_sh[f / BN][f % BN] = csum[i];
+      }
     }
     __syncthreads();
     for (int c = tid; c < BN; c += NT)

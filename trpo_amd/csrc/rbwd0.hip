@@ -307,12 +307,14 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
           }
         }
       };
-      // segment 0's product scale per 32-row tile (read before the first DMA: every ordinary load is consumed
-      // before the ring starts, or hipcc would drain it at its first use)
+      // segment 0's scale exponents, one per 32-row x 32-column block of RD_1: lane tm * nkb + kb holds block
+      // (tm, kb) of this tile (read before the first DMA: every ordinary load is consumed before the ring
+      // starts, or hipcc would drain it at its first use)
       const int eP1 = eA1p1 + eB1;
-      int eg[TM];
+      const int ev = ln < TM * nkb ? A.eA0t[((t0 >> 5) + ln / nkb) * nkb + ln % nkb] : 0;
+      int sc[TM];   // the product scale exponent acc[tm] is at
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) eg[tm] = __builtin_amdgcn_readfirstlane(A.eA0t[(t0 >> 5) + tm]) + eB0;
+      for (int tm = 0; tm < TM; ++tm) sc[tm] = eP1;
       asm volatile("s_waitcnt vmcnt(0)");
       issue_b(0);
       issue_a(0);
@@ -335,18 +337,25 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
           compute_pl(t, std::false_type{});
         }
       }
-      // segment 1 -> segment 0's per-tile scale (exact powers of two), then segment 0
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) acc[tm][0] *= __builtin_ldexpf(1.0f, eg[tm] - eP1);
+      // segment 0: before each k-block the accumulator of row tile tm moves to that block's product scale
+      // when it differs (exact powers of two; a uniform branch, rarely taken between neighbouring blocks)
       for (int t = ns1; t < nst; ++t) {
         top(t);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const int target = __builtin_amdgcn_readlane(ev, tm * nkb + (t - ns1)) + eB0;
+          if (target != sc[tm]) {
+            acc[tm][0] *= __builtin_ldexpf(1.0f, target - sc[tm]);
+            sc[tm] = target;
+          }
+        }
         compute_pl(t, std::false_type{});
       }
       // the X image takes the ring's bytes: every wave is past its last fragment read first
       __syncthreads();
       x_dma();
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) acc[tm][0] *= __builtin_ldexpf(1.0f, -eg[tm]);
+      for (int tm = 0; tm < TM; ++tm) acc[tm][0] *= __builtin_ldexpf(1.0f, -sc[tm]);
       if (Mt < kR0Rows) {
         // rows past the tile's end (the next split's, or past the shard) hold whatever the ring had: zero them
 #pragma unroll

@@ -109,7 +109,7 @@ __device__ __forceinline__ int sw_off(int mat, int plane, int j, int k) {
   return ((mat * 2 + plane) * 32 + j) * kTailK + (((k >> 3) ^ (j & 15)) << 3) + (k & 7);
 }
 
-// PL: RD_out as f16 planes with per-tile scales (TailArgs::RDh) instead of f32
+// PL: RD_out as f16 planes with a scale per 32 x 32 block (TailArgs::RDh) instead of f32
 template <bool PL>
 __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) {
   __shared__ __attribute__((aligned(16))) unsigned short sW[2 * 2 * 32 * kTailK];   // 64 KB
@@ -122,7 +122,6 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
   // (4 rows per wave) and read back as A fragments (ds_read_b128) and transposed (tr16)
   __shared__ __attribute__((aligned(16))) unsigned short sP[2 * 2 * TR * 32];
   __shared__ float sMax[2][NW];
-  __shared__ float sTm[2][NW];   // per-wave max |RD_out| of the tile (plane output's tile scale)
   __shared__ float sBias[NW][64];
   __shared__ float sOut[NW];
   if (A.skip && *A.skip) return;
@@ -374,10 +373,37 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
         mw = fmaxf(mw, fabsf(o));
       }
     }
-    if (planes) {
+    // ---- RD_out as f16 planes, one power-of-two scale per 32-row x 32-column block (this wave's): the
+    //      values come back from the wave's own LDS bytes (same-wave LDS order, no barrier).  Rows
+    //      (i&3)+8(i>>2)+4lh, column 32w + lr: register pairs (i, i+1) are rows r, r+1; lanes 2j, 2j+1 swap
+    //      one value each so that the even lane holds row r and the odd lane row r+1, both at columns 2j,
+    //      2j+1: one 4-byte store per plane and pair ----
+    if (planes && wv) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) mw = fmaxf(mw, __shfl_xor(mw, off, 64));
-      if (lane == 0) sTm[par][w] = mw;
+      const int et = f16_scale_exp(mw);
+      const float st = __builtin_ldexpf(1.0f, et);
+      if (lane == 0) A.eRD[(t0 / TR) * (apad / 32) + w] = et;
+      const int nr = max(0, min(TR, r1 - t0));
+      auto pdesc = [&](uint16_t* p) {   // k-block w of the tile: rows t0 .. t0 + nr, 64 B each
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + ((size_t)w * A.rd_mpad + t0) * 32), 0, nr * 64,
+                                                 0x00020000);
+      };
+      const __amdgpu_buffer_rsrc_t rHi = pdesc(A.RDh), rLo = pdesc(A.RDl);
+      const bool odd = lane & 1;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const float oi = ow[i * 64 + lane], oj = ow[(i + 1) * 64 + lane];
+        const float send = odd ? oi : oj;
+        const float recv = __shfl_xor(send, 1, 64);
+        const float a = (odd ? recv : oi) * st, bb = (odd ? oj : recv) * st;
+        const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, bb);
+        const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], bb - (float)hp[1]);
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * lh + (odd ? 1 : 0);
+        const int vo = (row * 32 + (lr & ~1)) * 2;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hp), rHi, vo, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lp), rLo, vo, 0, 0);
+      }
     }
     // ---- weight R-gradient: G += RH^T D_L + H^T RD_L (rows are the MFMA k).  B fragments (lane =
     //      action, element e of k-step s = row 16s + 8(e>>2) + 4lh + (e&3)) by transposed reads of
@@ -409,42 +435,6 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
       const float fG0 = __builtin_ldexpf(1.0f, -(eRH + eD)), fG1 = __builtin_ldexpf(1.0f, -(eH + eRD));
 #pragma unroll
       for (int i = 0; i < 16; ++i) G[i] += g0[i] * fG0 + g1[i] * fG1;
-    }
-
-    // ---- RD_out as f16 planes: the tile's scale needs every wave's max (published before the G
-    //      products, read after this barrier).  Rows (i&3)+8(i>>2)+4lh, column 32w + lr: register pairs
-    //      (i, i+1) are rows r, r+1; lanes 2j, 2j+1 swap one value each so that the even lane holds row r
-    //      and the odd lane row r+1, each at columns 2j, 2j+1: one 4-byte store per plane and pair ----
-    if (planes) {
-      lds_barrier();
-      float mt = 0.0f;
-#pragma unroll
-      for (int u = 0; u < NW; ++u) mt = fmaxf(mt, sTm[par][u]);
-      const int et = f16_scale_exp(mt);
-      const float st = __builtin_ldexpf(1.0f, et);
-      if (tid == 0) A.eRD[t0 / TR] = et;
-      const int nr = max(0, min(TR, r1 - t0));
-      auto pdesc = [&](uint16_t* p) {   // k-block w of the tile: rows t0 .. t0 + nr, 64 B each
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + ((size_t)w * A.rd_mpad + t0) * 32), 0, nr * 64,
-                                                 0x00020000);
-      };
-      const __amdgpu_buffer_rsrc_t rHi = pdesc(A.RDh), rLo = pdesc(A.RDl);
-      const bool odd = lane & 1;
-      if (wv) {
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const float oi = ow[i * 64 + lane], oj = ow[(i + 1) * 64 + lane];
-          const float send = odd ? oi : oj;
-          const float recv = __shfl_xor(send, 1, 64);
-          const float a = (odd ? recv : oi) * st, bb = (odd ? oj : recv) * st;
-          const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, bb);
-          const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], bb - (float)hp[1]);
-          const int row = (i & 3) + 8 * (i >> 2) + 4 * lh + (odd ? 1 : 0);
-          const int vo = (row * 32 + (lr & ~1)) * 2;
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hp), rHi, vo, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lp), rLo, vo, 0, 0);
-        }
-      }
     }
 
     if (t0 + TR < r1) {
