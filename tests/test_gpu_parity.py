@@ -282,7 +282,6 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"planes": 0},                                            # register-staged split instead of the plane kernel
     {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
-    {"rd_planes": 0}, {"rd_planes": 0, "chain": 0},           # f32 RD_1 between the tail and rbwd0
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -290,7 +289,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
-                                           "low_seg", "planes", "tail", "rbwd0", "rd_planes")}
+                                           "low_seg", "planes", "tail", "rbwd0")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -798,48 +797,3 @@ def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
         assert_vec_close(theta, r.theta_new, REL, f"theta rbwd0={mode}")
     assert_vec_close(out[1][0], out[0][0], REL, "fused vs per-layer Hv")
     assert_vec_close(out[1][1], out[0][1], REL, "fused vs per-layer g")
-
-
-@pytest.mark.parametrize("obs,hidden,A,n,low_seg", [
-    (128, [256, 256], 18, 3001, 14),     # C4 dims, ragged last tile
-    (128, [256, 256], 18, 40037, 14),    # several splits, a partial 128-row tile in each
-    (128, [256, 256], 18, 3001, 0),      # segment 1 on three products from D_1's hi / lo planes
-    (37, [192, 192], 17, 2500, 14),      # K = 192: three 64-deep one-product stages, 6 k-blocks
-], ids=["c4_dims", "many_splits", "three_products", "k192"])
-def test_rd_planes_vs_f32_and_oracle(gpu_available, obs, hidden, A, n, low_seg):
-    """RD_1 as the tail's per-32-row-tile-scaled f16 planes (tail.hip), streamed by LDS-DMA in rbwd0.hip and
-    unscaled on load by the layer-1 weight gradient (round 4), against the f32 RD_1 path (rd_planes = 0)
-    and the float64 oracle: Hv, a whole update (trpo_inksci.py:56-70,144-158)."""
-    from trpo_amd import Engine, UpdateParams
-    from trpo_amd._lib import get_option, set_option
-    spec = O.PolicySpec(obs, hidden, A)
-    dd = O.synthetic_batch(spec, n, seed=n + 3)
-    th = dd["theta"].astype(np.float64)
-    v = np.random.RandomState(n + 1).standard_normal(spec.n_params).astype(np.float32)
-    ref = O.fvp_undamped(th, dd["X"], v.astype(np.float64), spec)
-    r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
-    saved = {k: get_option(k) for k in ("rd_planes", "low_seg")}
-    out = {}
-    try:
-        set_option("low_seg", low_seg)
-        for mode in (1, 0):
-            set_option("rd_planes", mode)
-            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
-            e.set_flat(dd["theta"])
-            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
-            hv = e.fvp(v, 0.0)
-            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
-            out[mode] = (hv, st, e.get_flat())
-            e.close()
-    finally:
-        for k, val in saved.items():
-            set_option(k, val)
-    for mode in (1, 0):
-        hv, st, theta = out[mode]
-        assert_vec_close(hv, ref, REL, f"Hv rd_planes={mode}")
-        assert st["k"] == r.k
-        assert_vec_close(theta, r.theta_new, REL, f"theta rd_planes={mode}")
-    assert_vec_close(out[1][0], out[0][0], REL, "planes vs f32 RD_1 Hv")
-    # the two paths round differently (per-tile f16 hi + lo against f32): equal bits would mean the planes
-    # path did not run
-    assert not np.array_equal(out[1][0], out[0][0])

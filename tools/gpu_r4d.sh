@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+OUT=gpurun_out/${1:-r4d}; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "rd_planes or rbwd0 or tail or saturated or bench_dims" > $OUT/pytest_rd.log 2>&1
+rc=$?; tail -3 $OUT/pytest_rd.log; [ $rc -eq 0 ] || exit $rc
+bash tools/ab_env.sh ${1:-r4d}/ab c4 2 "TRPO_RD_PLANES=1" "TRPO_RD_PLANES=0"
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-alt --profile-out $OUT/events_c4.json > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail $OUT/bench_c4.err; exit 1; }

@@ -115,7 +115,6 @@ struct trpo_engine {
   uint16_t* D1h = nullptr;
   int d1_mpad = 0, d1_ldp = 0;
   bool d1_plane = false;   // D1h holds the current D_1
-  bool d1_lo = false;      // ... and D1l its lo plane
   int x_mpad = 0, x_ldp = 0;
   bool x_planes = false;   // Xh/Xl hold the current X
   bool planes_geom_l0() const {   // layer 0's row GEMMs fit the plane kernel
@@ -136,17 +135,6 @@ struct trpo_engine {
     sg.mpad = x_mpad;
     sg.eAp = pl_e;
     sg.Bb = dst;
-  }
-  // RD_1 as per-tile-scaled f16 planes (two hidden layers, fused tail + fused layer-1 R-backward): the tail
-  // writes them instead of f32 RD_1, the fused R-backward streams them (with D_1's hi / lo planes and k-blocked
-  // W_1^T / V_1^T planes) by LDS-DMA, the layer-1 weight gradient unscales them on load (round 4)
-  uint16_t *RDh = nullptr, *RDl = nullptr, *D1l = nullptr, *W1Tb = nullptr, *V1Tb = nullptr;
-  int* eRD = nullptr;
-  int rd_mpad = 0;
-  bool use_rd_planes() const {
-    return RDh && g_options.rd_planes != 0 && L == 3 && use_tail() && use_rbwd0() && d1_plane && d1_lo &&
-           !use_fused() && g_options.split_wg != 0 && w[2] > 128 &&   // layer 1's wgrad on the split tile (gemm.hip)
-           !use_chain() && wp[2] % 64 == 0 && r16(wp[2]) % 32 == 0;
   }
   uint16_t* tail_planes = nullptr;   // head planes of the fused FVP tail (tail.hip), [2][2][32][kTailK]
   // the fused last-layer tail: f16 split, last hidden width in (128, 256], 17..32 actions
@@ -402,15 +390,6 @@ struct trpo_engine {
     if (f16 && L >= 2 && rbwd0_geom()) {
       d1_ldp = (wp[2] + 31) / 32 * 32;
       D1h = dalloc<uint16_t>((size_t)((cap + 255) / 256 * 256) * d1_ldp);
-    }
-    if (f16 && L == 3 && rbwd0_geom() && tail_eligible(wp[2], wp[3]) && wp[2] % 64 == 0) {
-      rd_mpad = (int)((cap + 255) / 256 * 256);
-      RDh = dalloc<uint16_t>((size_t)rd_mpad * wp[2]);
-      RDl = dalloc<uint16_t>((size_t)rd_mpad * wp[2]);
-      D1l = dalloc<uint16_t>((size_t)((cap + 255) / 256 * 256) * d1_ldp);
-      eRD = dalloc<int>(((size_t)rd_mpad / 32 + 8) * (wp[2] / 32));   // one per 32 x 32 block
-      W1Tb = dalloc<uint16_t>(2 * plane3_b(1));
-      V1Tb = dalloc<uint16_t>(2 * plane3_b(1));
     }
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
@@ -897,12 +876,9 @@ struct trpo_engine {
     if (D1h && use_rbwd0() && n > 0) {
       d1_mpad = (int)((n + 255) / 256 * 256);
       Scope sp(this, "split_d1");
-      // the lo plane too where the fused R-backward streams planes (its three-product fallback reads it)
-      launch_split_planes(D[1], (int)n, d1_mpad, wp[2], wp[2], D1h, D1l && g_options.rd_planes ? D1l : nullptr,
-                          d1_ldp, am_d(1), pl_e + 1, stream);
+      launch_split_planes(D[1], (int)n, d1_mpad, wp[2], wp[2], D1h, nullptr, d1_ldp, am_d(1), pl_e + 1, stream);
       check_launch();
       d1_plane = true;
-      d1_lo = D1l && g_options.rd_planes;
     }
     reduce_losses(0, nullptr);
     prepared = true;
@@ -1012,13 +988,6 @@ struct trpo_engine {
     split_parts(false, true, false, true, WF, WF3, skip, "split_v");
     am_reset(am_rh(0), L);
     am_reset(am_rd(0), L);
-    const bool rdp = use_rd_planes();
-    if (rdp) {
-      // k-blocked copies of the W_1^T / V_1^T planes for the fused R-backward's DMA ring
-      launch_block_planes(WB3[1], 2, wp[1], r16(wp[2]), W1Tb, stream);
-      launch_block_planes(WB3[1] + 3 * plane3_b(1), 2, wp[1], r16(wp[2]), V1Tb, stream);
-      check_launch();
-    }
     // R-forward (the fused tail takes the last layer's)
     const bool tail = use_tail();
     const int Lf = tail ? L - 1 : L;
@@ -1098,12 +1067,6 @@ struct trpo_engine {
       ta.am_v = am_v(l);
       ta.am_out = am_rd(l - 1);
       ta.RDout = RD[l - 1];
-      if (rdp) {
-        ta.RDh = RDh;
-        ta.RDl = RDl;
-        ta.rd_mpad = rd_mpad;
-        ta.eRD = eRD;
-      }
       ta.invN = 1.0 / (double)n_global;
       ta.splits = active_splits;
       ta.rows_per_split = rows_per_split;
@@ -1139,15 +1102,6 @@ struct trpo_engine {
           a.am_a1 = am_d(1);
           a.E = E[0];
           a.RH = RH[1];
-          if (rdp) {
-            a.A0h = RDh;
-            a.A0l = RDl;
-            a.a0_mpad = rd_mpad;
-            a.eA0t = eRD;
-            a.A1l = D1l;
-            a.B0b = W1Tb;
-            a.B1b = V1Tb;
-          }
           Scope sp(this, "fvp_rbwdwg_l1");
           launch_rbwd0(a, stream);
           check_launch();
@@ -1185,16 +1139,9 @@ struct trpo_engine {
         std::snprintf(tag, sizeof tag, "fvp_wgrad_l%d", l);
         if (l == 0)
           wgrad_layer(0, 1, WSeg{X, RD[0], wp[0], wp[1], am_x(), am_rd(0)}, WSeg{}, 0, skip, tag);
-        else {
-          WSeg s1{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)};
-          if (rdp && l == 1) {   // RD_1 exists only as the tail's planes
-            s1.Bh = RDh;
-            s1.Bl = RDl;
-            s1.b_mpad = rd_mpad;
-            s1.eBt = eRD;
-          }
-          wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)}, s1, 1, skip, tag);
-        }
+        else
+          wgrad_layer(l, 2, WSeg{RH[l], D[l], wp[l], wp[l + 1], am_rh(l), am_d(l)},
+                      WSeg{H[l], RD[l], wp[l], wp[l + 1], nullptr, am_rd(l)}, 1, skip, tag);
       }
     };
     r_backward();
@@ -2363,7 +2310,6 @@ static int* option_slot(const std::string& k) {
   if (k == "low_seg") return &g_options.low_seg;
   if (k == "planes") return &g_options.planes;
   if (k == "rbwd0") return &g_options.rbwd0;
-  if (k == "rd_planes") return &g_options.rd_planes;
   throw ArgError("unknown option " + k);
 }
 

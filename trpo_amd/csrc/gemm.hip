@@ -37,7 +37,7 @@ static int env_int(const char* name, int dflt) {
 Options g_options = {env_int("TRPO_SPLIT_MFMA", 5), env_int("TRPO_SPLIT_WG", 1), env_int("TRPO_CHAIN", 1),
                      env_int("TRPO_SPLIT_F16", 1), env_int("TRPO_SPLIT_MIN_K", 0), env_int("TRPO_GRAPHS", 1),
                      env_int("TRPO_TAIL", 1), env_int("TRPO_FUSED", 2), env_int("TRPO_LOW_SEG", 14),
-                     env_int("TRPO_PLANES", 1), env_int("TRPO_RBWD0", 1), env_int("TRPO_RD_PLANES", 1)};
+                     env_int("TRPO_PLANES", 1), env_int("TRPO_RBWD0", 1)};
 
 namespace {
 
@@ -555,23 +555,11 @@ wgrad3_kernel(const WGradArgs args) {
   auto ldbuf = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
   };
-  // segments whose B is a plane pair with per-block scales (WSeg::Bh): thread tid < BN loads columns 2p, 2p + 1
-  // (p = tid % (BN / 2)) of 8-row group tid / (BN / 2), one 4-byte load per plane and row
-  const int pp = tid % (BN / 2), pg = tid / (BN / 2);
-  const int pcol = n0 + 2 * pp;
-  const bool pok = pcol < args.Npad;
-  // offsets reach 3.6 GB at C4 (past int32): unsigned bits, with an all-ones out-of-range sentinel
-  const int vBp = (int)(pok ? (unsigned)((((int64_t)(pcol >> 5) * args.seg[1].b_mpad + 8 * pg) * 32 + (pcol & 31)) * 2)
-                            : 0xFFFFFFF0u);
-
   struct Stage {
     float va[AP][8], vb[BP][8];
-    float vp[2][8];  // a plane segment (WSeg::Bh): threads tid < BN hold columns 2p, 2p + 1 of their 8 rows
     bool cs;         // this tile belongs to the column-summed segment
     int sg;          // segment
-    bool pl;         // the tile's B comes from planes
   };
-  float csp[2] = {0.0f, 0.0f};   // plane segments' column sums (columns 2p, 2p + 1)
   auto gload = [&](Stage& st, int t) {
     const int sg = t / nk;
     const int kt = t - sg * nk;
@@ -587,37 +575,10 @@ wgrad3_kernel(const WGradArgs args) {
     for (int i = 0; i < AP; ++i)
 #pragma unroll
       for (int q = 0; q < 8; ++q) st.va[i][q] = ldbuf(ra, vA[i], sa + q * lda4);
-    const WSeg& sgw = sg ? args.seg[1] : args.seg[0];
-    st.pl = NP == 2 && sgw.Bh != nullptr;
-    if (NP == 2 && sgw.Bh) {
-      // (hi + lo) 2^-e of the lane's 32 x 32 block (k-tiles of 16 rows never straddle a block row:
-      // r0 % 32 == 0); rows past the split (another split's, or past the shard) are zeroed
-      if (tid < BN) {
-        const int nkbB = args.Npad >> 5;
-        const int e = pok ? sgw.eBt[((r0 + kt * BK) >> 5) * nkbB + (pcol >> 5)] : 0;
-        const float inv = __builtin_ldexpf(1.0f, -e);
-        const unsigned nbytes = (unsigned)((((int64_t)(args.Npad - 1) >> 5) * sgw.b_mpad + (r1 - r0)) * 64);
-        const __amdgpu_buffer_rsrc_t rh =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bh + (size_t)r0 * 32), 0, nbytes, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rl =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(sgw.Bl + (size_t)r0 * 32), 0, nbytes, 0x00020000);
-        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int so = (kt * BK + q) * 64;
-          const h2 hv = __builtin_bit_cast(h2, __builtin_amdgcn_raw_buffer_load_b32(rh, vBp, so, 0));
-          const h2 lv = __builtin_bit_cast(h2, __builtin_amdgcn_raw_buffer_load_b32(rl, vBp, so, 0));
-          const bool ok = r0 + kt * BK + 8 * pg + q < r1;
-          st.vp[0][q] = ok ? ((float)hv[0] + (float)lv[0]) * inv : 0.0f;
-          st.vp[1][q] = ok ? ((float)hv[1] + (float)lv[1]) * inv : 0.0f;
-        }
-      }
-    } else {
+    for (int i = 0; i < BP; ++i)
 #pragma unroll
-      for (int i = 0; i < BP; ++i)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) st.vb[i][q] = ldbuf(rb, vB[i], sb + q * ldb4);
-    }
+      for (int q = 0; q < 8; ++q) st.vb[i][q] = ldbuf(rb, vB[i], sb + q * ldb4);
     __builtin_amdgcn_sched_barrier(0);
   };
   auto put = [&](unsigned short* base, int plane_elems, int c, int g, const float (&v)[8], int e) {
@@ -656,21 +617,6 @@ wgrad3_kernel(const WGradArgs args) {
     for (int i = 0; i < AP; ++i) {
       const int f = tid + i * NT;
       if (AI % NT == 0 || f < AI) put(As, APL, f % BM, f / BM, st.va[i], eA[st.sg]);
-    }
-    if (NP == 2 && st.pl) {
-      if (tid < BN) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          put(Bs, BPL, 2 * pp + j, pg, st.vp[j], eB[st.sg]);
-          if (st.cs) {
-            float cs = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) cs += st.vp[j][q];
-            csp[j] += cs;
-          }
-        }
-      }
-      return;
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
@@ -810,18 +756,10 @@ wgrad3_kernel(const WGradArgs args) {
     }
   if (do_colsum) {
     // column sums: the two 8-row groups of a column, combined in a fixed order
-    const bool cs_planes = NP == 2 && args.seg[args.colsum_seg].Bh != nullptr;
-    if (cs_planes) {
-      if (tid < BN) {
-        cs_sh[pg][2 * pp] = csp[0];
-        cs_sh[pg][2 * pp + 1] = csp[1];
-      }
-    } else {
 #pragma unroll
-      for (int i = 0; i < BP; ++i) {
-        const int f = tid + i * NT;
-        if (BI % NT == 0 || f < BI) cs_sh[f / BN][f % BN] = csum[i];
-      }
+    for (int i = 0; i < BP; ++i) {
+      const int f = tid + i * NT;
+      if (BI % NT == 0 || f < BI) cs_sh[f / BN][f % BN] = csum[i];
     }
     __syncthreads();
     for (int c = tid; c < BN; c += NT)
@@ -1123,13 +1061,6 @@ void launch_wg3_cfg(const WGradArgs& a, hipStream_t s) {
     throw std::runtime_error("split-bf16 wgrad: segments with different leading dimensions");
   if ((int64_t)a.rows_per_split * (a.seg[0].lda > a.seg[0].ldb ? a.seg[0].lda : a.seg[0].ldb) * 4 >= (int64_t(1) << 30))
     throw std::runtime_error("split-bf16 wgrad: a split's rows exceed the 1 GiB buffer-descriptor range");
-  for (int i = 0; i < a.nseg; ++i) {
-    const WSeg& sg = a.seg[i];
-    if (!sg.Bh) continue;
-    if (!a.f16 || i != 1 || !sg.Bl || !sg.eBt || a.rows_per_split % 32 || sg.b_mpad < a.rows ||
-        (((int64_t)(a.Npad - 1) >> 5) * sg.b_mpad + a.rows_per_split) * 64 >= (int64_t(1) << 32) - 64)
-      throw std::runtime_error("split wgrad: B planes need f16, segment 1, 32-row splits and a 4 GiB range");
-  }
   dim3 grid((a.Ma + BM - 1) / BM, (a.Nb + BN - 1) / BN, a.splits);
   WGradArgs b = a;
   b.low_seg = g_options.low_seg;
@@ -1184,8 +1115,6 @@ void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
 void launch_wgrad(const WGradArgs& a, hipStream_t s) {
   if (a.splits <= 0) return;
   const int Mp = a.Ma, Np = a.Nb;
-  if ((a.seg[0].Bh || (a.nseg > 1 && a.seg[1].Bh)) && !(Np > 128 && g_options.split_wg != 0))
-    throw std::runtime_error("wgrad: B planes are read by the split weight-gradient tile only");
   // output tile by (fan_in, fan_out); every B column set of one split lives in one block row
   if (Np <= 32) {
     if (Mp <= 64) launch_wg_cfg<2, 1, 1, 1>(a, s);          // 64 x 32

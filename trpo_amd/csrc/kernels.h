@@ -28,8 +28,6 @@ struct Options {
                    // plane kernel (plane.hip): 0 off, 1 on
   int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
-  int rd_planes;   // engine: two hidden layers under the fused tail and rbwd0: RD_1 as per-tile-scaled f16 planes
-                   // (tail.hip writes, rbwd0.hip streams them by LDS-DMA, the weight gradient unscales): 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -168,12 +166,6 @@ struct WSeg {
   int lda, ldb;
   const unsigned* amaxA = nullptr;   // f16 split: max |A|, max |B| (float bits; NULL = bounded by 1)
   const unsigned* amaxB = nullptr;
-  // f16 split only: B as k-blocked f16 hi/lo planes (GemmSeg::Ah layout, row stride b_mpad) with one power-of-two
-  // scale 2^eBt[(r / 32) * (Npad / 32) + c / 32] per 32 x 32 block (TailArgs::RDh), read and unscaled to f32 in
-  // place of B (amaxB stays the global running max that sets the split scale)
-  const uint16_t *Bh = nullptr, *Bl = nullptr;
-  int b_mpad = 0;
-  const int* eBt = nullptr;
 };
 
 struct WGradArgs {
@@ -405,12 +397,6 @@ struct TailArgs {
   const unsigned *am_rh, *am_d, *am_w, *am_v;   // running-max slots of RH, D_L, W, V
   unsigned* am_out;           // running max |RD_out|
   float* RDout;               // [rows][apad]  R-delta into the last hidden layer (RD_{L-2})
-  // RDh != NULL: RD_{L-2} goes out instead as scaled f16 hi/lo planes, k-blocked (GemmSeg::Ah layout: element
-  // (r, k) at ((k / 32) * rd_mpad + r) * 32 + k % 32), (hi + lo) = RD 2^eRD[(r / 32) * (apad / 32) + k / 32]
-  // with one power-of-two scale per 32-row x 32-column block (its max in [2^11, 2^12)); RDout is not written
-  uint16_t *RDh = nullptr, *RDl = nullptr;
-  int rd_mpad = 0;
-  int* eRD = nullptr;
   double invN;
   int splits, rows_per_split; // rows_per_split % 32 == 0
   float* slab;
@@ -464,17 +450,6 @@ struct RBwd0Args {
   int64_t slab_stride, off_w, off_b;
   const int* skip;
   int low_seg = 0;          // f16: segment 1 on one product when it sits >= low_seg binades under (set at launch)
-  // planes form (two segments): every k-loop operand is a pre-split f16 plane brought in by LDS-DMA.
-  // Segment 0 = RD_1 as k-blocked hi/lo planes (GemmSeg::Ah layout, row stride a0_mpad) with one power-of-two
-  // scale 2^eA0t[(r / 32) * (ldk / 32) + k / 32] per 32 x 32 block (TailArgs::RDh); segment 1 = D_1's hi (A1h)
-  // and lo (A1l) planes,
-  // scale 2^(*eA1p); B = k-blocked copies of the W_1^T / V_1^T planes, [plane][ldk / 32][Npad][32]
-  // (launch_block_planes).  A0h != NULL selects it.
-  const uint16_t *A0h = nullptr, *A0l = nullptr;
-  int a0_mpad = 0;
-  const int* eA0t = nullptr;
-  const uint16_t* A1l = nullptr;
-  const uint16_t *B0b = nullptr, *B1b = nullptr;
 };
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s);

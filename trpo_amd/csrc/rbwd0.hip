@@ -70,15 +70,7 @@ constexpr int kR0BI = 2 * kR0BPL / 8 / kR0NT; // u16x8 B staging items per threa
 constexpr int kR0XP = 2 * kR0XPL * 2 / 1024;  // 1-KB X DMA pieces per tile (both planes)
 constexpr int kR0XD = kR0XP / kR0NW;          // ... per wave
 constexpr bool kR0XAlias = (2 * kR0STG + 2 * kR0XPL) * 2 + 64 > 160 * 1024;   // X image in the staging bytes
-constexpr int kR0LDSR = kR0XAlias ? (2 * kR0STG > 2 * kR0XPL ? 2 * kR0STG : 2 * kR0XPL) : 2 * kR0STG + 2 * kR0XPL;
-// planes form: a ring of kR0SA A stages (hi + lo sub-blocks of 128 rows x 32 k) and kR0SB B stages (256 columns
-// x 32 k), X's image aliasing it after the k-loop
-constexpr int kR0SA = 3, kR0SB = 2;
-constexpr int kR0PA = kR0Rows * 32;            // u16 per A sub-block
-constexpr int kR0PB = 256 * 32;                // u16 per B sub-block
-constexpr int kR0PLU = kR0SA * 2 * kR0PA + kR0SB * 2 * kR0PB;
-constexpr int kR0LDSU = kR0LDSR > kR0PLU ? kR0LDSR : kR0PLU;
-static_assert(kR0PLU >= 2 * kR0XPL && kR0Rows == 128 && kR0NW == 8, "rbwd0 planes-form ring");
+constexpr int kR0LDSU = kR0XAlias ? (2 * kR0STG > 2 * kR0XPL ? 2 * kR0STG : 2 * kR0XPL) : 2 * kR0STG + 2 * kR0XPL;
 static_assert(kR0LDSU * 2 <= 160 * 1024, "rbwd0 LDS");
 static_assert(kR0BK == 16 || kR0BK == 32, "rbwd0 k-tile");
 
@@ -140,9 +132,7 @@ __device__ __forceinline__ f32x16 mfma3h(const f16x8& ah, const f16x8& al, const
 // NSEG = 2: FVP ([RD_1 | D_1], with the E RH term); NSEG = 1: policy gradient (DS_1, no E term)
 // SW: segment 1 on one product from D_1's hi plane (decided per launch on the device, rbwd0_sw); the two
 // variants are separate instantiations so neither carries the other's live ranges
-// PL: the planes form (RBwd0Args::A0h): segment 1 first (one product on D_1's hi plane under SW, else three on
-// its hi / lo planes), then segment 0 from RD_1's per-tile-scaled planes, every operand by LDS-DMA
-template <int NSEG, bool SW, bool PL = false>
+template <int NSEG, bool SW>
 __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* smem, float* sMax) {
   constexpr bool kE = NSEG == 2;
   constexpr int TM = kR0TM, CT = kR0CT;
@@ -182,14 +172,13 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
   (void)one1;
   constexpr int sw = SW ? 1 : 0;   // rbwd0_sw: one1 with the plane and an even split of the k-loop
   const int eA1p = sw ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;
-  const int eA1p1 = PL ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;   // planes form: D_1's planes, either way
   const float sDown = __builtin_ldexpf(1.0f, sw ? eP - (eA1p + eB1) : 0);
   const int bbytes = (int)(2 * A.plane * 2);
 
   const unsigned xbytes = (unsigned)A.x_ldp * (unsigned)A.x_mpad * 2u;
   const __amdgpu_buffer_rsrc_t rXh = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xh, 0, xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rXl = __builtin_amdgcn_make_buffer_rsrc((void*)A.Xl, 0, xbytes, 0x00020000);
-  unsigned short* const sX = smem + ((kR0XAlias || PL) ? 0 : 2 * kR0STG);
+  unsigned short* const sX = smem + (kR0XAlias ? 0 : 2 * kR0STG);
   const unsigned lds_x = (unsigned)(uintptr_t)sX;
 
   // lane-dependent values are recomputed per tile from an opaque copy of the thread id: hoisted out of
@@ -230,7 +219,7 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
               lds_x + (unsigned)(pl * kR0XPL * 2 + (kb % (kR0XP / 2)) * 1024));
       }
     };
-    if (!kR0XAlias && !PL) x_dma();
+    if (!kR0XAlias) x_dma();
 
     // ---- k-loop: acc = [A0 | A1] [B0 ; B1] on the f16 split ----
     f32x16 acc[TM][CT];
@@ -238,133 +227,6 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < CT; ++j) acc[i][j] = f32x16{};
-    if constexpr (PL) {
-      // ---- planes form.  Stage t: segment 1 for t < ns1 (64 k of D_1's hi plane as two sub-blocks under
-      //      SW, else 32 k as hi + lo), then segment 0 (32 k of RD_1, hi + lo).  Wave wv moves sub-block
-      //      wv >> 2: A rows (wv & 3) * 32 .. + 32 (two 1-KB pieces), B columns (wv & 3) * 64 .. + 64 (four).
-      //      Issue order per step: B(t + 1), A(t + 2); at the top of step t only A(t + 1)'s two DMAs may stay
-      //      in flight (vmcnt(2)).  Rows past Mt are cut off by the descriptors and zeroed after the loop. ----
-      const int ns1 = sw ? K / 64 : K / 32, ns0 = K / 32, nst = ns1 + ns0;
-      const int nkb = A.ldk / 32;
-      const int sub = wv >> 2;
-      const int rows0 = (wv & 3) * 32, cols0 = (wv & 3) * 64;
-      const int ln = lane_of() & 63;
-      const unsigned voff = (unsigned)((ln >> 2) * 64 + 16 * ((ln & 3) ^ ((ln >> 4) & 3)));
-      const unsigned lds0 = (unsigned)(uintptr_t)smem;
-      const unsigned ldsA = lds0, ldsB = lds0 + (unsigned)(kR0SA * 2 * kR0PA * 2);
-      auto issue_a = [&](int t) {
-        const bool s1 = t < ns1;
-        const bool one = s1 && sw;
-        const int kb = s1 ? (one ? 2 * t + sub : t) : t - ns1;
-        const uint16_t* p = s1 ? ((one || sub == 0) ? A.A1h : A.A1l) : (sub == 0 ? A.A0h : A.A0l);
-        const int mp = s1 ? A.a1_mpad : A.a0_mpad;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p + ((size_t)kb * mp + t0) * 32), 0, (unsigned)(Mt * 64), 0x00020000);
-        const unsigned dst = ldsA + (unsigned)(((t % kR0SA) * 2 + sub) * kR0PA * 2 + rows0 * 64);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) dma16(rs, voff + (unsigned)((rows0 + 16 * i) * 64), dst + 1024u * i);
-      };
-      auto issue_b = [&](int t) {
-        const bool s1 = t < ns1;
-        const bool one = s1 && sw;
-        const int kb = s1 ? (one ? 2 * t + sub : t) : t - ns1;
-        const int pl = one ? 0 : sub;
-        const uint16_t* p = (s1 ? A.B1b : A.B0b) + (((size_t)pl * nkb + kb) * Npad + cols0) * 32;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 4096u, 0x00020000);
-        const unsigned dst = ldsB + (unsigned)(((t % kR0SB) * 2 + sub) * kR0PB * 2 + cols0 * 64);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dma16(rs, voff + 1024u * i, dst + 1024u * i);
-      };
-      auto compute_pl = [&](int t, auto one_c) {
-        constexpr bool ONE = decltype(one_c)::value;
-        const unsigned short* As = smem + (t % kR0SA) * 2 * kR0PA;
-        const unsigned short* Bs = smem + kR0SA * 2 * kR0PA + (t % kR0SB) * 2 * kR0PB;
-        const int n = col0 + lr;
-        if constexpr (ONE) {
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int sb = ks >> 1, c = 2 * (ks & 1) + lh;
-            const f16x8 bh = *reinterpret_cast<const f16x8*>(Bs + sb * kR0PB + swzk(n, c));
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-              const f16x8 ah = *reinterpret_cast<const f16x8*>(As + sb * kR0PA + swzk(32 * tm + lr, c));
-              acc[tm][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[tm][0], 0, 0, 0);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const int c = 2 * ks + lh;
-            const f16x8 bh = *reinterpret_cast<const f16x8*>(Bs + swzk(n, c));
-            const f16x8 bl = *reinterpret_cast<const f16x8*>(Bs + kR0PB + swzk(n, c));
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-              const int ao = swzk(32 * tm + lr, c);
-              const f16x8 ah = *reinterpret_cast<const f16x8*>(As + ao);
-              const f16x8 al = *reinterpret_cast<const f16x8*>(As + kR0PA + ao);
-              acc[tm][0] = mfma3h(ah, al, bh, bl, acc[tm][0]);
-            }
-          }
-        }
-      };
-      // segment 0's scale exponents, one per 32-row x 32-column block of RD_1: lane tm * nkb + kb holds block
-      // (tm, kb) of this tile (read before the first DMA: every ordinary load is consumed before the ring
-      // starts, or hipcc would drain it at its first use)
-      const int eP1 = eA1p1 + eB1;
-      const int ev = ln < TM * nkb ? A.eA0t[((t0 >> 5) + ln / nkb) * nkb + ln % nkb] : 0;
-      int sc[TM];   // the product scale exponent acc[tm] is at
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) sc[tm] = eP1;
-      asm volatile("s_waitcnt vmcnt(0)");
-      issue_b(0);
-      issue_a(0);
-      if (1 < nst) issue_a(1);
-      auto top = [&](int t) {
-        if (t + 1 < nst) asm volatile("s_waitcnt vmcnt(2)");
-        else asm volatile("s_waitcnt vmcnt(0)");
-        __syncthreads();   // stage t visible to every wave; stage t - 1's slots are free
-        if (t + 1 < nst) issue_b(t + 1);
-        if (t + 2 < nst) issue_a(t + 2);
-      };
-      if (sw) {
-        for (int t = 0; t < ns1; ++t) {
-          top(t);
-          compute_pl(t, std::true_type{});
-        }
-      } else {
-        for (int t = 0; t < ns1; ++t) {
-          top(t);
-          compute_pl(t, std::false_type{});
-        }
-      }
-      // segment 0: before each k-block the accumulator of row tile tm moves to that block's product scale
-      // when it differs (exact powers of two; a uniform branch, rarely taken between neighbouring blocks)
-      for (int t = ns1; t < nst; ++t) {
-        top(t);
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          const int target = __builtin_amdgcn_readlane(ev, tm * nkb + (t - ns1)) + eB0;
-          if (target != sc[tm]) {
-            acc[tm][0] *= __builtin_ldexpf(1.0f, target - sc[tm]);
-            sc[tm] = target;
-          }
-        }
-        compute_pl(t, std::false_type{});
-      }
-      // the X image takes the ring's bytes: every wave is past its last fragment read first
-      __syncthreads();
-      x_dma();
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) acc[tm][0] *= __builtin_ldexpf(1.0f, -sc[tm]);
-      if (Mt < kR0Rows) {
-        // rows past the tile's end (the next split's, or past the shard) hold whatever the ring had: zero them
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int rr = 0; rr < 16; ++rr)
-            if (32 * tm + (rr & 3) + 8 * (rr >> 2) + 4 * lh >= Mt) acc[tm][0][rr] = 0.0f;
-      }
-    } else {
     struct Stage {
       f32x4 ra[kR0AI];
       u16x8 rb[kR0BI];
@@ -544,7 +406,6 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
 #pragma unroll
         for (int j = 0; j < CT; ++j) acc[i][j] *= f;
     }
-    }   // register-staged form
 
     // ---- epilogue: RD_0 = acc (1 - H^2) + E RH in place (rows past the split read 0: RD_0 = 0) ----
     {
@@ -690,7 +551,7 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
 __device__ __forceinline__ bool rbwd0_sw(const RBwd0Args& A) {
   if (kR0BK != 32 || A.nseg < 2 || !A.A1h || A.low_seg <= 0) return false;
   const int nk = (A.K + kR0BK - 1) / kR0BK;
-  if (!A.A0h && nk % R0_PF) return false;
+  if (nk % R0_PF) return false;
   const int q0 = amax_exp(A.am_a0) + amax_exp(A.am_b0), q1 = amax_exp(A.am_a1) + amax_exp(A.am_b1);
   const int pen0 = (!A.am_a0 || !A.am_b0) ? 4 : 0;
   return __builtin_amdgcn_readfirstlane(q1 - q0 >= A.low_seg + pen0 ? 1 : 0) != 0;
@@ -702,11 +563,6 @@ __global__ void __launch_bounds__(kR0NT, 1) rbwd0_kernel(const RBwd0Args A) {
   __shared__ float sMax[kR0NW];
   if (A.skip && *A.skip) return;
   if constexpr (NSEG > 1) {
-    if (A.A0h) {
-      if (rbwd0_sw(A)) rbwd0_body<NSEG, true, true>(A, smem, sMax);
-      else rbwd0_body<NSEG, false, true>(A, smem, sMax);
-      return;
-    }
     if (rbwd0_sw(A)) {
       rbwd0_body<NSEG, true>(A, smem, sMax);
       return;

@@ -109,8 +109,6 @@ __device__ __forceinline__ int sw_off(int mat, int plane, int j, int k) {
   return ((mat * 2 + plane) * 32 + j) * kTailK + (((k >> 3) ^ (j & 15)) << 3) + (k & 7);
 }
 
-// PL: RD_out as f16 planes with a scale per 32 x 32 block (TailArgs::RDh) instead of f32
-template <bool PL>
 __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) {
   __shared__ __attribute__((aligned(16))) unsigned short sW[2 * 2 * 32 * kTailK];   // 64 KB
   // per wave 8 KB: the tile's RH / H f16 planes as [mat][plane][k][m] images for the transposed
@@ -348,16 +346,11 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
       aDV = mfma3(dh_, dl_, vt[s][0], vt[s][1], aDV);
       aDW = mfma3(dh_, dl_, wt[s][0], wt[s][1], aDW);
     }
-    // ---- RD = RDH (1 - H^2) + E RH, E = -2 DH H (gemm.hip kPrepBwd / kRBwd).  For the plane output the
-    //      values wait in the wave's own sX bytes (free from here to the next tile's head R-forward) for
-    //      the tile scale instead of in registers ----
-    constexpr bool planes = PL;
-    float* ow = reinterpret_cast<float*>(sX[w]);
-    float mw = 0.0f;   // this wave's max |RD_out| over the tile (plane output)
+    // ---- RD = RDH (1 - H^2) + E RH, E = -2 DH H (gemm.hip kPrepBwd / kRBwd) ----
     {
       const float fRW = __builtin_ldexpf(1.0f, -(eRD + eW)), fDV = __builtin_ldexpf(1.0f, -(eD + eV));
       const float fDW = __builtin_ldexpf(1.0f, -(eD + eW));
-      const __amdgpu_buffer_rsrc_t rOut = desc(planes ? A.H : A.RDout, t0, apad);
+      const __amdgpu_buffer_rsrc_t rOut = desc(A.RDout, t0, apad);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float rdh = aRW[i] * fRW + aDV[i] * fDV;
@@ -365,44 +358,9 @@ __global__ void __launch_bounds__(NW * 64, 1) fvp_tail_kernel(const TailArgs A) 
         const float h = cH[i], rh = cRH[i];
         const float e = -2.0f * dh * h;
         const float o = fmaf(e, rh, rdh * omsq(h));
-        if (planes) ow[i * 64 + lane] = o;
-        else
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rOut, vo_c,
-                                                ((i & 3) + 8 * (i >> 2)) * apad * 4, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rOut, vo_c,
+                                              ((i & 3) + 8 * (i >> 2)) * apad * 4, 0);
         mxo = fmaxf(mxo, fabsf(o));
-        mw = fmaxf(mw, fabsf(o));
-      }
-    }
-    // ---- RD_out as f16 planes, one power-of-two scale per 32-row x 32-column block (this wave's): the
-    //      values come back from the wave's own LDS bytes (same-wave LDS order, no barrier).  Rows
-    //      (i&3)+8(i>>2)+4lh, column 32w + lr: register pairs (i, i+1) are rows r, r+1; lanes 2j, 2j+1 swap
-    //      one value each so that the even lane holds row r and the odd lane row r+1, both at columns 2j,
-    //      2j+1: one 4-byte store per plane and pair ----
-    if (planes && wv) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) mw = fmaxf(mw, __shfl_xor(mw, off, 64));
-      const int et = f16_scale_exp(mw);
-      const float st = __builtin_ldexpf(1.0f, et);
-      if (lane == 0) A.eRD[(t0 / TR) * (apad / 32) + w] = et;
-      const int nr = max(0, min(TR, r1 - t0));
-      auto pdesc = [&](uint16_t* p) {   // k-block w of the tile: rows t0 .. t0 + nr, 64 B each
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + ((size_t)w * A.rd_mpad + t0) * 32), 0, nr * 64,
-                                                 0x00020000);
-      };
-      const __amdgpu_buffer_rsrc_t rHi = pdesc(A.RDh), rLo = pdesc(A.RDl);
-      const bool odd = lane & 1;
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const float oi = ow[i * 64 + lane], oj = ow[(i + 1) * 64 + lane];
-        const float send = odd ? oi : oj;
-        const float recv = __shfl_xor(send, 1, 64);
-        const float a = (odd ? recv : oi) * st, bb = (odd ? oj : recv) * st;
-        const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, bb);
-        const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], bb - (float)hp[1]);
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * lh + (odd ? 1 : 0);
-        const int vo = (row * 32 + (lr & ~1)) * 2;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hp), rHi, vo, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lp), rLo, vo, 0, 0);
       }
     }
     // ---- weight R-gradient: G += RH^T D_L + H^T RD_L (rows are the MFMA k).  B fragments (lane =
@@ -510,13 +468,7 @@ void launch_fvp_tail(const TailArgs& a, hipStream_t s) {
     throw std::runtime_error("fvp_tail: unsupported layer shape");
   if (a.splits <= 0) return;
   if (a.rows_per_split % TR) throw std::runtime_error("fvp_tail: rows_per_split % 32");
-  if (a.RDh) {
-    if (!a.RDl || !a.eRD || a.rd_mpad < a.rows || a.rd_mpad % 32 || a.apad % 32)
-      throw std::runtime_error("fvp_tail: plane output without its planes / exponents");
-    hipLaunchKernelGGL(fvp_tail_kernel<true>, dim3(a.splits), dim3(NW * 64), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(fvp_tail_kernel<false>, dim3(a.splits), dim3(NW * 64), 0, s, a);
-  }
+  hipLaunchKernelGGL(fvp_tail_kernel, dim3(a.splits), dim3(NW * 64), 0, s, a);
 }
 
 }  // namespace trpo
