@@ -282,6 +282,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"planes": 0},                                            # register-staged split instead of the plane kernel
     {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
+    {"hbwd2": 0}, {"hbwd2": 0, "chain": 0},                   # separate head backwards (prepare / policy gradient)
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -289,7 +290,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
-                                           "low_seg", "planes", "tail", "rbwd0")}
+                                           "low_seg", "planes", "tail", "rbwd0", "hbwd2")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -797,3 +798,48 @@ def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
         assert_vec_close(theta, r.theta_new, REL, f"theta rbwd0={mode}")
     assert_vec_close(out[1][0], out[0][0], REL, "fused vs per-layer Hv")
     assert_vec_close(out[1][1], out[0][1], REL, "fused vs per-layer g")
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (128, [256, 256], 18, 3001),       # C4 dims, ragged last tile (D_1's hi plane per 32-row tile)
+    (128, [256, 256], 18, 40037),      # several splits
+    (37, [192, 200], 17, 2500),        # K = 200 for the fused R-backward, 17 actions
+    (64, [256, 256, 256], 32, 900),    # depth 3: D_2 / DS_2 (no hi plane), A = 32
+], ids=["c4_dims", "many_splits", "odd", "depth3"])
+def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
+    """hbwd.hip: the prepare pass's D_{L-2} and the policy gradient's DS_{L-2} in one read of H (and D_1's f16 hi
+    plane scaled per 32-row tile) against the two row-GEMM backwards (option hbwd2 = 0) and the float64 oracle:
+    g, Hv and a whole update (trpo_inksci.py:54,56-70,144-158)."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + 5)
+    th = dd["theta"].astype(np.float64)
+    v = np.random.RandomState(n + 2).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(th, dd["X"], v.astype(np.float64), spec)
+    gref = O.policy_grad(th, dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
+    saved = get_option("hbwd2")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("hbwd2", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            g = e.policy_grad()
+            hv = e.fvp(v, 0.0)
+            g2 = e.policy_grad()          # after an FVP wrote RD: the policy gradient recomputes DS_{L-2}
+            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out[mode] = (g, hv, g2, st, e.get_flat())
+            e.close()
+    finally:
+        set_option("hbwd2", saved)
+    for mode in (1, 0):
+        g, hv, g2, st, theta = out[mode]
+        assert_vec_close(g, gref, REL, f"g hbwd2={mode}")
+        assert_vec_close(g2, gref, REL, f"g after fvp hbwd2={mode}")
+        assert_vec_close(hv, ref, REL, f"Hv hbwd2={mode}")
+        assert st["k"] == r.k
+        assert_vec_close(theta, r.theta_new, REL, f"theta hbwd2={mode}")
+    assert_vec_close(out[1][0], out[0][0], REL, "dual vs row-GEMM backward g")

@@ -115,6 +115,15 @@ struct trpo_engine {
   uint16_t* D1h = nullptr;
   int d1_mpad = 0, d1_ldp = 0;
   bool d1_plane = false;   // D1h holds the current D_1
+  bool d1_tiled = false;   // ... with one scale per 32-row tile (eD1t, hbwd.hip) instead of pl_e[1]
+  int* eD1t = nullptr;
+  // the prepare pass also produced the policy gradient's DS_{L-2} (hbwd.hip, in RD[L-2]); any launch that
+  // writes RD clears it
+  bool ds_ready = false;
+  bool use_hbwd2() const {
+    // the head layer's backward is the D-only (kPgBwd) step: a hidden layer below it, E_{L-2} not read
+    return g_options.hbwd2 != 0 && L >= 3 && head_bwd2_eligible(w[L], wp[L - 1]) && !e_top_needed();
+  }
   int x_mpad = 0, x_ldp = 0;
   bool x_planes = false;   // Xh/Xl hold the current X
   bool planes_geom_l0() const {   // layer 0's row GEMMs fit the plane kernel
@@ -390,6 +399,7 @@ struct trpo_engine {
     if (f16 && L >= 2 && rbwd0_geom()) {
       d1_ldp = (wp[2] + 31) / 32 * 32;
       D1h = dalloc<uint16_t>((size_t)((cap + 255) / 256 * 256) * d1_ldp);
+      eD1t = dalloc<int>((size_t)(cap + 31) / 32 + 8);
     }
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
@@ -849,9 +859,47 @@ struct trpo_engine {
     // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
     // recomputes it from H and D_{L-1}.
     prep_e_top = e_top_needed();
+    ds_ready = false;
+    d1_plane = false;
+    d1_tiled = false;
+    const bool hb2 = use_hbwd2();
     for (int l = L - 1; l >= 1; --l) {
       const bool need_d = l > 1, need_e = l < L - 1 || prep_e_top;
       if (!need_d && !need_e) continue;
+      if (l == L - 1 && hb2) {
+        // D_{L-2} and the policy gradient's DS_{L-2} in one read of H_{L-1} (hbwd.hip), with D_1's hi plane for
+        // the fused R-backward where it runs (two hidden layers), scaled per 32-row tile
+        am_reset(am_ds(L - 2), 1);
+        HeadBwd2Args hb{};
+        hb.rows = (int)n;
+        hb.A = w[L];
+        hb.Apad = wp[L];
+        hb.N = w[L - 1];
+        hb.Npad = wp[L - 1];
+        hb.WB = WB[L - 1];
+        hb.D2 = D[L - 1];
+        hb.DS2 = DSL;
+        hb.H = H[L - 1];
+        hb.D1 = D[L - 2];
+        hb.DS1 = RD[L - 2];
+        hb.am_d1 = am_d(L - 2);
+        hb.am_ds1 = am_ds(L - 2);
+        if (L == 3 && D1h && eD1t && use_rbwd0() && wp[2] % 32 == 0 && n > 0) {
+          d1_mpad = (int)((n + 255) / 256 * 256);
+          hb.D1h = D1h;
+          hb.d1_mpad = d1_mpad;
+          hb.eD1t = eD1t;
+        }
+        Scope sp(this, "bwd2_l2");
+        launch_head_bwd2(hb, num_cus, stream);
+        check_launch();
+        ds_ready = true;
+        if (hb.D1h) {
+          d1_plane = true;
+          d1_tiled = true;
+        }
+        continue;
+      }
       RowGemmArgs a = row_args(w[l], wp[l]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{D[l], WB[l], wp[l + 1], wp[l], wp[l + 1]};
@@ -872,8 +920,7 @@ struct trpo_engine {
       check_launch();
     }
     // D_1's hi plane for the fused R-backward (per update; the FVPs' D_1 V_1^T segment reads half the bytes)
-    d1_plane = false;
-    if (D1h && use_rbwd0() && n > 0) {
+    if (!d1_plane && D1h && use_rbwd0() && n > 0) {
       d1_mpad = (int)((n + 255) / 256 * 256);
       Scope sp(this, "split_d1");
       launch_split_planes(D[1], (int)n, d1_mpad, wp[2], wp[2], D1h, nullptr, d1_ldp, am_d(1), pl_e + 1, stream);
@@ -926,9 +973,10 @@ struct trpo_engine {
     std::vector<float*> DS(L);
     DS[L - 1] = DSL;
     for (int l = 0; l < L - 1; ++l) DS[l] = RD[l];
-    am_reset(am_ds(0), L - 1);
+    const bool have_ds = ds_ready;   // DS_{L-2} (and its running max) from the prepare pass (hbwd.hip)
+    am_reset(am_ds(0), have_ds ? L - 2 : L - 1);
     const bool r0f = use_rbwd0();
-    for (int l = L - 1; l >= 1; --l) {
+    for (int l = have_ds ? L - 2 : L - 1; l >= 1; --l) {
       if (l == 1 && r0f) {
         // DS_0 stays in registers: X^T DS_0 and its column sums go straight to the slab (rbwd0.hip)
         RBwd0Args a = rbwd0_args(nullptr);
@@ -971,6 +1019,7 @@ struct trpo_engine {
     // the path changed since prepare(): E_{L-2} needed but not written
     if (prepared && e_top_needed() && !prep_e_top) prepared = false;
     prepare();
+    ds_ready = false;   // the FVP's R-backward writes RD (DS_{L-2}'s scratch)
     if (use_fused()) {
       fvp_fused(v, out, skip);
       return;
@@ -1097,6 +1146,7 @@ struct trpo_engine {
             a.A1h = D1h;
             a.a1_mpad = d1_mpad;
             a.eA1p = pl_e + 1;
+            if (d1_tiled) a.eA1t = eD1t;
           }
           a.am_a0 = am_rd(1);
           a.am_a1 = am_d(1);
@@ -1412,7 +1462,7 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top;
+    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready;
   } upd_flags{};
   void drop_graph() {
     if (upd_exec) {
@@ -1440,6 +1490,7 @@ struct trpo_engine {
       chain_w_valid = upd_flags.chain_w_valid;
       have_returns = upd_flags.have_returns;
       prep_e_top = upd_flags.prep_e_top;
+      ds_ready = upd_flags.ds_ready;
       return;
     }
     if (!same) {
@@ -1474,7 +1525,7 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top};
+    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;
@@ -2310,6 +2361,7 @@ static int* option_slot(const std::string& k) {
   if (k == "low_seg") return &g_options.low_seg;
   if (k == "planes") return &g_options.planes;
   if (k == "rbwd0") return &g_options.rbwd0;
+  if (k == "hbwd2") return &g_options.hbwd2;
   throw ArgError("unknown option " + k);
 }
 

@@ -28,6 +28,8 @@ struct Options {
                    // plane kernel (plane.hip): 0 off, 1 on
   int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
+  int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
+                   // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -431,6 +433,7 @@ struct RBwd0Args {
   const float* A0;          // [rows][lda] RD_1 (or DS_1)
   const float* A1;          // [rows][lda] D_1
   const uint16_t* A1h;      // D_1's k-blocked f16 hi plane (GemmSeg::Ah layout, scale 2^(*eA1p)); NULL: none
+  const int* eA1t = nullptr;   // ... or, when set, one scale 2^eA1t[r / 32] per 32-row tile (hbwd.hip)
   int a1_mpad;
   const int* eA1p;
   const uint16_t* B0;       // f16 hi/lo planes of W_1^T: [2][Npad][ldk] (plane stride `plane`)
@@ -451,6 +454,27 @@ struct RBwd0Args {
   const int* skip;
   int low_seg = 0;          // f16: segment 1 on one product when it sits >= low_seg binades under (set at launch)
 };
+// The prepare pass's and the policy gradient's backward through the head layer in one read of H (hbwd.hip):
+//   D1 = (D2 W^T)(1 - H^2), DS1 = (DS2 W^T)(1 - H^2)  (K = n_actions <= 32), optionally D1's f16 hi plane
+// (GemmSeg::Ah layout, row stride d1_mpad, scale 2^eD1t[r / 32] per 32-row tile)
+struct HeadBwd2Args {
+  int rows;
+  int A, Apad;              // actions; leading dimension of D2 / DS2
+  int N, Npad;              // last hidden width; leading dimension of H / D1 / DS1
+  const float* WB;          // W^T rows [0, A) of the packed backward operand, [.][Npad]
+  const float* D2;
+  const float* DS2;
+  const float* H;
+  float* D1;
+  float* DS1;
+  unsigned* am_d1;
+  unsigned* am_ds1;
+  uint16_t* D1h = nullptr;
+  int d1_mpad = 0;
+  int* eD1t = nullptr;
+};
+bool head_bwd2_eligible(int A, int Npad);
+void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s);
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s);
 void launch_tail_pack(const TailPackArgs& p, hipStream_t s);

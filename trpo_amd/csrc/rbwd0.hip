@@ -171,8 +171,9 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
   // segment 0. Without the plane (or with a k-tile count the unrolled loop cannot split) both run 3 products.
   (void)one1;
   constexpr int sw = SW ? 1 : 0;   // rbwd0_sw: one1 with the plane and an even split of the k-loop
-  const int eA1p = sw ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;
-  const float sDown = __builtin_ldexpf(1.0f, sw ? eP - (eA1p + eB1) : 0);
+  // the plane's scale: one exponent (*eA1p) or one per 32-row tile (eA1t, hbwd.hip: row tile tm of a 128-row
+  // tile steps down by its own power of two)
+  const int eA1p = (sw && !A.eA1t) ? __builtin_amdgcn_readfirstlane(*A.eA1p) : 0;
   const int bbytes = (int)(2 * A.plane * 2);
 
   const unsigned xbytes = (unsigned)A.x_ldp * (unsigned)A.x_mpad * 2u;
@@ -335,6 +336,11 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
       // segment 1's one-product tiles [0, t1) and the 3-product tiles [t1, ntiles) as two loops (t1 a multiple
       // of the unroll): their bodies differ in the compute step, and a branch there inside one loop spills
       const int t1 = sw ? nk : 0;
+      // the D_1 plane's scale exponent of each 32-row tile (uniform: scalar registers across the k-loop)
+      int e1s[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        e1s[i] = (sw && A.eA1t) ? __builtin_amdgcn_readfirstlane(A.eA1t[(t0 >> 5) + i]) : eA1p;
 #if R0_PF == 4
       // four k-tiles of loads in flight: stage S_(j % 4) holds k-tile j from its load, issued three steps
       // ahead, until its LDS store
@@ -388,10 +394,14 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
       };
 #endif
       kloop(0, t1, std::true_type{});
+      if (sw) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+          const float f = __builtin_ldexpf(1.0f, eP - (e1s[i] + eB1));
 #pragma unroll
-        for (int j = 0; j < CT; ++j) acc[i][j] *= sDown;
+          for (int j = 0; j < CT; ++j) acc[i][j] *= f;
+        }
+      }
       kloop(t1, ntiles, std::false_type{});
     }
     if (kR0XAlias) {
