@@ -884,6 +884,12 @@ struct trpo_engine {
         hb.DS1 = RD[L - 2];
         hb.am_d1 = am_d(L - 2);
         hb.am_ds1 = am_ds(L - 2);
+        hb.splits = active_splits;
+        hb.rows_per_split = rows_per_split;
+        hb.slab = slab;   // the policy gradient's W_{L-1} / b_{L-1} block, reduced by policy_grad()
+        hb.slab_stride = slab_stride;
+        hb.off_w = offW[L - 1];
+        hb.off_b = offb[L - 1];
         if (L == 3 && D1h && eD1t && use_rbwd0() && wp[2] % 32 == 0 && n > 0) {
           d1_mpad = (int)((n + 255) / 256 * 256);
           hb.D1h = D1h;
@@ -1005,7 +1011,8 @@ struct trpo_engine {
       launch_rowgemm(a, stream);
       check_launch();
     }
-    for (int l = r0f ? 1 : 0; l < L; ++l) {
+    // with DS_{L-2} from the prepare pass the head layer's weight gradient is already in the slabs
+    for (int l = r0f ? 1 : 0; l < (have_ds ? L - 1 : L); ++l) {
       char t[32];
       std::snprintf(t, sizeof t, "pg_wgrad_l%d", l);
       wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1], l == 0 ? am_x() : nullptr, am_ds(l)}, WSeg{}, 0,

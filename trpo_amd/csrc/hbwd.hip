@@ -34,10 +34,19 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
 #pragma unroll
   for (int j = 0; j < AT; ++j) w[j] = (cv && j < a.A) ? a.WB[(size_t)j * a.Npad + c] : 0.0f;
   float mx1 = 0.0f, mx2 = 0.0f;
-  const int ntiles = (a.rows + kHbRows - 1) / kHbRows;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int t0 = tile * kHbRows;
-    const int nr = min(kHbRows, a.rows - t0);
+  // the policy gradient's last-layer weight gradient over this split's rows (slab != NULL): gw[j] = sum_r H[r][c]
+  // DS2[r][j], column c's row of the W block, and the bias column sum of DS2 (thread j < A)
+  const bool wg = a.slab != nullptr;
+  float gw[AT];
+#pragma unroll
+  for (int j = 0; j < AT; ++j) gw[j] = 0.0f;
+  float gb = 0.0f;
+  // workgroup s walks split s's rows (the weight-gradient slabs' partition, engine set_splits)
+  const int r0 = blockIdx.x * a.rows_per_split;
+  const int r1 = min(a.rows, r0 + a.rows_per_split);
+  for (int t0 = r0; t0 < r1; t0 += kHbRows) {
+    const int tile = t0 / kHbRows;
+    const int nr = min(kHbRows, r1 - t0);
     __syncthreads();   // the previous tile's deltas and values are consumed
     for (int i = c; i < 2 * kHbRows * AT; i += kHbThreads) {
       const int m = i / (kHbRows * AT), r = (i / AT) % kHbRows, j = i % AT;
@@ -63,6 +72,14 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
       if (r < nr && cv) {
         const size_t idx = (size_t)(t0 + r) * a.Npad + c;
         const float h = a.H[idx];
+        if (wg) {
+#pragma unroll
+          for (int j = 0; j < AT; j += 4) {
+            const f32x4 y = *reinterpret_cast<const f32x4*>(&sd[1][r][j]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gw[j + q] = fmaf(h, y[q], gw[j + q]);
+          }
+        }
         const float om = (1.0f - h) * (1.0f + h);
         o1 = d * om;
         const float o2 = s * om;
@@ -73,6 +90,7 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
         tm = fmaxf(tm, fabsf(o1));
       }
       sv[r][c] = o1;
+      if (wg && c < a.A && r < nr) gb += sd[1][r][c];
     }
     if (a.D1h) {
       // the tile's scale: max |D| over its rows and every column
@@ -91,6 +109,15 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
         for (int r = 0; r < nr; ++r) dst[(size_t)r * 32] = __builtin_bit_cast(unsigned short, (_Float16)(sv[r][c] * sc));
       }
     }
+  }
+  if (wg) {
+    float* out = a.slab + (size_t)blockIdx.x * a.slab_stride;
+    if (c < a.N) {
+#pragma unroll
+      for (int j = 0; j < AT; ++j)
+        if (j < a.A) out[a.off_w + (int64_t)c * a.A + j] = gw[j];
+    }
+    if (c < a.A) out[a.off_b + c] = gb;
   }
   // running maxima of both outputs (the f16 split scales of their consumers): one atomicMax per workgroup
 #pragma unroll
@@ -125,8 +152,10 @@ void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s) {
     throw std::runtime_error("head_bwd2: unsupported shape or missing operand");
   if (a.D1h && (!a.eD1t || a.d1_mpad < a.rows || a.Npad % 32))
     throw std::runtime_error("head_bwd2: hi plane without its exponents or stride");
-  const int ntiles = (a.rows + kHbRows - 1) / kHbRows;
-  const int grid = ntiles < 4 * num_cus ? ntiles : 4 * num_cus;
+  (void)num_cus;
+  if (a.splits <= 0 || a.rows_per_split % kHbRows || (int64_t)a.splits * a.rows_per_split < a.rows)
+    throw std::runtime_error("head_bwd2: splits do not cover the rows in 32-row tiles");
+  const int grid = a.splits;
   switch ((a.A + 3) / 4) {
     case 1: hipLaunchKernelGGL(head_bwd2_kernel<4>, dim3(grid), dim3(kHbThreads), 0, s, a); break;
     case 2: hipLaunchKernelGGL(head_bwd2_kernel<8>, dim3(grid), dim3(kHbThreads), 0, s, a); break;

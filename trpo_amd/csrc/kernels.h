@@ -455,7 +455,8 @@ struct RBwd0Args {
   int low_seg = 0;          // f16: segment 1 on one product when it sits >= low_seg binades under (set at launch)
 };
 // The prepare pass's and the policy gradient's backward through the head layer in one read of H (hbwd.hip):
-//   D1 = (D2 W^T)(1 - H^2), DS1 = (DS2 W^T)(1 - H^2)  (K = n_actions <= 32), optionally D1's f16 hi plane
+//   D1 = (D2 W^T)(1 - H^2), DS1 = (DS2 W^T)(1 - H^2)  (K = n_actions <= 32), the policy gradient's head-layer
+// weight gradient H^T DS2 (+ bias colsum) into the slabs, optionally D1's f16 hi plane
 // (GemmSeg::Ah layout, row stride d1_mpad, scale 2^eD1t[r / 32] per 32-row tile)
 struct HeadBwd2Args {
   int rows;
@@ -472,6 +473,12 @@ struct HeadBwd2Args {
   uint16_t* D1h = nullptr;
   int d1_mpad = 0;
   int* eD1t = nullptr;
+  // workgroup s takes the rows of split s (the weight-gradient slab partition); slab != NULL: it also writes the
+  // policy gradient's last-layer weight gradient (H^T DS2, W block [N][A] at off_w, bias colsum DS2 at off_b) of
+  // its rows into slab s
+  int splits = 0, rows_per_split = 0;
+  float* slab = nullptr;
+  int64_t slab_stride = 0, off_w = 0, off_b = 0;
 };
 bool head_bwd2_eligible(int A, int Npad);
 void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s);
