@@ -789,6 +789,38 @@ struct trpo_engine {
       a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
       a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
       if (l == 0 && planes_l0()) attach_x_planes(a.seg[0], wf3[0], W0b);
+      if (l == L - 1 && g_options.head_fwd != 0 && head_fwd_eligible(w[L], w[L - 1]) &&
+          (head == RowEpi::kPrepHead || head == RowEpi::kLossHead)) {
+        // the softmax head with one state per lane (hbwd.hip): bound by its read of H_{L-1}
+        HeadFwdArgs hf{};
+        hf.rows = n;
+        hf.A = w[L];
+        hf.Apad = wp[L];
+        hf.K = w[l];
+        hf.Kpad = wp[l];
+        hf.H = l == 0 ? X : hout[l];
+        hf.W = wf[l];
+        hf.bias = th + offb[l];
+        hf.old = old;
+        hf.act = act;
+        hf.adv = adv32;
+        hf.rowterms = rowterms;
+        hf.invN = 1.0 / (double)n_global;
+        if (head == RowEpi::kPrepHead) {
+          hf.prep = 1;
+          hf.P = Pm;
+          hf.D = D[L - 1];
+          hf.DS = DSL;
+          hf.am_d = am_d(L - 1);
+          hf.am_ds = am_ds(L - 1);
+        }
+        char t[32];
+        std::snprintf(t, sizeof t, "%s_l%d", tag, l);
+        Scope sp(this, t);
+        launch_head_fwd(hf, num_cus, stream);
+        check_launch();
+        continue;
+      }
       a.ea.bias = th + offb[l];
       a.ea.ldo = wp[l + 1];
       if (l < L - 1) {
@@ -2369,6 +2401,7 @@ static int* option_slot(const std::string& k) {
   if (k == "planes") return &g_options.planes;
   if (k == "rbwd0") return &g_options.rbwd0;
   if (k == "hbwd2") return &g_options.hbwd2;
+  if (k == "head_fwd") return &g_options.head_fwd;
   throw ArgError("unknown option " + k);
 }
 

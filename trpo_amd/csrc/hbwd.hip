@@ -13,6 +13,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <stdexcept>
 
 namespace trpo {
@@ -47,6 +48,12 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
   for (int t0 = r0; t0 < r1; t0 += kHbRows) {
     const int tile = t0 / kHbRows;
     const int nr = min(kHbRows, r1 - t0);
+    // the tile's own weight-gradient partials, added to the split's sums once per tile: a split is ~15k rows
+    // at C4, and one f32 running sum over all of them would carry ~sqrt(n) roundings
+    float tw[AT];
+#pragma unroll
+    for (int j = 0; j < AT; ++j) tw[j] = 0.0f;
+    float tb = 0.0f;
     __syncthreads();   // the previous tile's deltas and values are consumed
     for (int i = c; i < 2 * kHbRows * AT; i += kHbThreads) {
       const int m = i / (kHbRows * AT), r = (i / AT) % kHbRows, j = i % AT;
@@ -77,7 +84,7 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
           for (int j = 0; j < AT; j += 4) {
             const f32x4 y = *reinterpret_cast<const f32x4*>(&sd[1][r][j]);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) gw[j + q] = fmaf(h, y[q], gw[j + q]);
+            for (int q = 0; q < 4; ++q) tw[j + q] = fmaf(h, y[q], tw[j + q]);
           }
         }
         const float om = (1.0f - h) * (1.0f + h);
@@ -90,7 +97,12 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
         tm = fmaxf(tm, fabsf(o1));
       }
       sv[r][c] = o1;
-      if (wg && c < a.A && r < nr) gb += sd[1][r][c];
+      if (wg && c < a.A && r < nr) tb += sd[1][r][c];
+    }
+    if (wg) {
+#pragma unroll
+      for (int j = 0; j < AT; ++j) gw[j] += tw[j];
+      gb += tb;
     }
     if (a.D1h) {
       // the tile's scale: max |D| over its rows and every column
@@ -166,6 +178,197 @@ void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s) {
     case 7: hipLaunchKernelGGL(head_bwd2_kernel<28>, dim3(grid), dim3(kHbThreads), 0, s, a); break;
     default: hipLaunchKernelGGL(head_bwd2_kernel<32>, dim3(grid), dim3(kHbThreads), 0, s, a); break;
   }
+}
+
+}  // namespace trpo
+
+// =============================================================================================================
+// Softmax head forward, one state per lane (gfx950): z = H_{L-1} W_L + b_L (K = last hidden width, N = n_actions
+// <= 32), p = softmax(z) and the row terms of surr / kl / ent (trpo_inksci.py:38-53), plus for the prepare pass
+// the KL_ff plain logit delta D_L and the surr logit delta DS_L (cancellation-free forms, as gemm.hip's kPrepHead
+// row epilogue).  K <= 256 and N <= 32 make the product a few thousand FMAs per state: the launch is bound by its
+// read of H, so it runs on f32 VALU FMAs with the state's whole softmax row in one lane (no cross-lane sums), the
+// H tile staged through LDS in 32-column chunks (the next chunk's loads in flight during the current one's FMAs).
+// =============================================================================================================
+namespace trpo {
+namespace {
+
+constexpr int kHfRows = 256;   // states per tile (one per thread)
+constexpr int kHfK = 32;       // columns of H per chunk
+constexpr int kHfLd = kHfK + 1;
+
+template <int AT, bool PREP>
+__global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) {
+  __shared__ float sH[kHfRows * kHfLd];
+  __shared__ __attribute__((aligned(16))) float sW[kHfK][AT];
+  __shared__ float sred[2][kHfRows / 64];
+  const int t = threadIdx.x;
+  const int nchunk = (a.K + kHfK - 1) / kHfK;
+  float mD = 0.0f, mS = 0.0f;
+  for (int64_t t0 = (int64_t)blockIdx.x * kHfRows; t0 < a.rows; t0 += (int64_t)gridDim.x * kHfRows) {
+    const int nr = (int)min<int64_t>(kHfRows, a.rows - t0);
+    // chunk loads: thread t moves float4 q of rows t / 8 + 32 q, columns 4 (t % 8) .. + 3 of the chunk
+    f32x4 nx[8];
+    auto load_chunk = [&](int c) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = t / 8 + 32 * q, col = kHfK * c + 4 * (t % 8);
+        nx[q] = (r < nr && col < a.Kpad) ? *reinterpret_cast<const f32x4*>(a.H + (t0 + r) * a.Kpad + col)
+                                         : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    };
+    float acc[AT];
+#pragma unroll
+    for (int j = 0; j < AT; ++j) acc[j] = 0.0f;
+    load_chunk(0);
+    for (int c = 0; c < nchunk; ++c) {
+      __syncthreads();   // the previous chunk's reads are done
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = t / 8 + 32 * q, col = 4 * (t % 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sH[r * kHfLd + col + e] = nx[q][e];
+      }
+      for (int i = t; i < kHfK * AT; i += kHfRows) {
+        const int k = i / AT, j = i % AT, kk = kHfK * c + k;
+        sW[k][j] = (kk < a.K && j < a.A) ? a.W[(size_t)kk * a.Apad + j] : 0.0f;
+      }
+      __syncthreads();
+      if (c + 1 < nchunk) load_chunk(c + 1);
+#pragma unroll 8
+      for (int k = 0; k < kHfK; ++k) {
+        const float h = sH[t * kHfLd + k];
+#pragma unroll
+        for (int j = 0; j < AT; j += 4) {
+          const f32x4 w4 = *reinterpret_cast<const f32x4*>(&sW[k][j]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[j + e] = fmaf(h, w4[e], acc[j + e]);
+        }
+      }
+    }
+    if (t < nr) {
+      const int64_t row = t0 + t;
+      const float* oldr = a.old + row * a.Apad;
+      float z[AT], p[AT];
+      float zm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < AT; ++j) {
+        z[j] = j < a.A ? acc[j] + a.bias[j] : -INFINITY;
+        zm = fmaxf(zm, z[j]);
+      }
+      float es = 0.0f;
+#pragma unroll
+      for (int j = 0; j < AT; ++j) {
+        p[j] = j < a.A ? expf(z[j] - zm) : 0.0f;
+        es += p[j];
+      }
+#pragma unroll
+      for (int j = 0; j < AT; ++j) p[j] = p[j] / es;
+      const int av = a.act[row];
+      const float adv = a.adv[row];
+      float pa = 0.0f, olda = 0.0f;
+      double klp = 0.0, enp = 0.0;
+#pragma unroll
+      for (int j = 0; j < AT; ++j) {
+        if (j < a.A) {
+          const float oj = oldr[j];
+          if (j == av) {
+            pa = p[j];
+            olda = oj;
+          }
+          // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs, f64 row sums
+          klp += (double)oj * (double)logf((oj + kEps) / (p[j] + kEps));
+          enp += -(double)p[j] * (double)logf(p[j] + kEps);
+        }
+      }
+      double* rt = a.rowterms + 4 * row;
+      rt[0] = (double)pa / (double)olda * (double)adv;
+      rt[1] = klp;
+      rt[2] = enp;
+      rt[3] = 0.0;
+      if constexpr (PREP) {
+        // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps); surr logit delta
+        // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead)
+        double B[AT], spB = 0.0, rest = 0.0;
+#pragma unroll
+        for (int j = 0; j < AT; ++j) {
+          const double pd = p[j];
+          B[j] = j < a.A ? (double)kEps / (pd + (double)kEps) : 0.0;
+          spB += pd * B[j];
+          rest += (j < a.A && j != av) ? pd : 0.0;
+        }
+        const double coef = -(double)adv * a.invN / (double)olda * (double)pa;
+        float* Pr = a.P + row * a.Apad;
+        float* Dr = a.D + row * a.Apad;
+        float* Sr = a.DS + row * a.Apad;
+#pragma unroll
+        for (int j = 0; j < AT; ++j) {
+          if (j < a.Apad) {
+            const bool real = j < a.A;
+            const double pd = p[j];
+            const float dl = real ? (float)(pd * a.invN * (B[j] - spB)) : 0.0f;
+            const float ds = real ? (float)(coef * (j == av ? rest : -pd)) : 0.0f;
+            Pr[j] = real ? p[j] : 0.0f;
+            Dr[j] = dl;
+            Sr[j] = ds;
+            mD = fmaxf(mD, fabsf(dl));
+            mS = fmaxf(mS, fabsf(ds));
+          }
+        }
+      }
+    }
+  }
+  if constexpr (PREP) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      mD = fmaxf(mD, __shfl_xor(mD, off, 64));
+      mS = fmaxf(mS, __shfl_xor(mS, off, 64));
+    }
+    __syncthreads();
+    if ((t & 63) == 0) {
+      sred[0][t >> 6] = mD;
+      sred[1][t >> 6] = mS;
+    }
+    __syncthreads();
+    if (t < 2) {
+      unsigned* slot = t == 0 ? a.am_d : a.am_ds;
+      if (slot) {
+        float m = 0.0f;
+#pragma unroll
+        for (int u = 0; u < kHfRows / 64; ++u) m = fmaxf(m, sred[t][u]);
+        if (m > 0.0f) atomicMax(slot + (blockIdx.x % kAmaxSub) * kAmaxStride, __float_as_uint(m));
+      }
+    }
+  }
+}
+
+template <bool PREP>
+void launch_head_fwd_t(const HeadFwdArgs& a, int grid, hipStream_t s) {
+  switch ((a.A + 3) / 4) {
+    case 1: hipLaunchKernelGGL((head_fwd_kernel<4, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((head_fwd_kernel<8, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((head_fwd_kernel<12, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((head_fwd_kernel<16, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((head_fwd_kernel<20, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((head_fwd_kernel<24, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((head_fwd_kernel<28, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+    default: hipLaunchKernelGGL((head_fwd_kernel<32, PREP>), dim3(grid), dim3(kHfRows), 0, s, a); break;
+  }
+}
+
+}  // namespace
+
+bool head_fwd_eligible(int A, int K) { return A <= 32 && K >= 1 && K <= 4096; }
+
+void launch_head_fwd(const HeadFwdArgs& a, int num_cus, hipStream_t s) {
+  if (a.rows <= 0) return;
+  if (!head_fwd_eligible(a.A, a.K) || a.Apad < a.A || a.Kpad < a.K || a.Kpad % 4 || !a.H || !a.W || !a.bias ||
+      !a.old || !a.act || !a.adv || !a.rowterms || (a.prep && (!a.P || !a.D || !a.DS)))
+    throw std::runtime_error("head_fwd: unsupported shape or missing operand");
+  const int64_t tiles = (a.rows + kHfRows - 1) / kHfRows;
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)4 * num_cus);
+  if (a.prep) launch_head_fwd_t<true>(a, grid, s);
+  else launch_head_fwd_t<false>(a, grid, s);
 }
 
 }  // namespace trpo

@@ -30,6 +30,8 @@ struct Options {
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
   int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
                    // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
+  int head_fwd;    // engine: the softmax head forward (prepare and line search) with one state per lane on f32 FMAs
+                   // (hbwd.hip) instead of the f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -481,6 +483,29 @@ struct HeadBwd2Args {
   int64_t slab_stride = 0, off_w = 0, off_b = 0;
 };
 bool head_bwd2_eligible(int A, int Npad);
+// The softmax head forward with one state per lane (hbwd.hip): z = H W + b (K = last hidden width, A <= 32 actions),
+// p = softmax(z), the surr / kl / ent row terms, and with prep also P, D_L, DS_L (gemm.hip kPrepHead semantics)
+struct HeadFwdArgs {
+  int64_t rows;
+  int A, Apad;              // actions; leading dimension of old / P / D / DS and of W's rows
+  int K, Kpad;              // last hidden width; leading dimension of H
+  const float* H;
+  const float* W;           // [K][Apad] (the packed forward operand's W half)
+  const float* bias;        // [A]
+  const float* old;
+  const int* act;
+  const float* adv;
+  double* rowterms;         // [rows][4]
+  double invN;
+  int prep = 0;
+  float* P = nullptr;
+  float* D = nullptr;
+  float* DS = nullptr;
+  unsigned* am_d = nullptr;
+  unsigned* am_ds = nullptr;
+};
+bool head_fwd_eligible(int A, int K);
+void launch_head_fwd(const HeadFwdArgs& a, int num_cus, hipStream_t s);
 void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s);
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s);
