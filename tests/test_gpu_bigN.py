@@ -15,31 +15,29 @@ n_global = 8M scaling through a row slice the oracle does evaluate:
 * arithmetic    f16x3 split vs the exact bf16x6 split on the same 8M batch (norm-relative 1e-5)
 * slice         3000 rows with n_global = 8M against the float64 oracle (SURVEY.md §8(d) bar)
 * whole update  the bench's full update at 8M (discount, standardise, pg, 10 CG, shs, line search) on its
-                own arithmetic (f16x3 + one-product low segment) vs three products everywhere and vs the
-                exact bf16x6 split: g, stepdir, fullstep, theta_new at 1e-5, CG count and k exact
+                own arithmetic (f16x3 + one-product low segment), on three products everywhere and on the
+                exact bf16x6 split, against the same update in float64 (oracle/chunked_f64.py in a child
+                process): CG count and k exact, vectors at max(1e-5, 2 x float32's own error)
 """
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
+from bign_data import N, SPEC, make_batch, make_rewards
 from conftest import assert_vec_close, rel_l2
 from oracle import trpo_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-N = 8_000_000
-SPEC = O.PolicySpec(128, [256, 256], 18)
 REL = 1e-5
 
 
 @pytest.fixture(scope="module")
 def big_batch():
-    rng = np.random.default_rng(0)
-    X = rng.standard_normal((N, SPEC.obs_dim), dtype=np.float32)
-    actions = rng.integers(0, SPEC.n_actions, N, dtype=np.int64)
-    theta = O.init_theta(SPEC, np.random.RandomState(1)).astype(np.float32)
-    u = np.random.RandomState(2).standard_normal(SPEC.n_params).astype(np.float32)
-    v = np.random.RandomState(3).standard_normal(SPEC.n_params).astype(np.float32)
-    return {"X": X, "actions": actions, "theta": theta, "u": u, "v": v}
+    return make_batch()
 
 
 def _engine(b, rows=None, n_global=N):
@@ -148,29 +146,50 @@ def _update_8m(b, opts):
 
 @pytest.fixture(scope="module")
 def updates_8m(big_batch, hv_f16):
-    rng = np.random.default_rng(5)
-    big_batch["rewards"] = rng.random(N)
-    big_batch["starts"] = (np.arange(N) % 200 == 0).astype(np.uint8)   # CartPole-v0 path length cap
+    big_batch["rewards"], big_batch["starts"] = make_rewards()
     return {"default": _update_8m(big_batch, {}),
             "low_seg=0": _update_8m(big_batch, {"low_seg": 0}),
             "bf16x6": _update_8m(big_batch, {"split_f16": 0})}
 
 
-@pytest.mark.parametrize("variant", ["low_seg=0", "bf16x6"])
-def test_c4_8m_whole_update_arithmetic(gpu_available, updates_8m, variant):
-    """The bench's headline update at its full size on the arithmetic the number is measured with
-    (f16x3 split + one-product low segment) against (a) three products everywhere and (b) the exact
-    bf16 hi+mid+lo split (6 products): g, stepdir, fullstep, theta_new at 1e-5; shs and the losses at
-    1e-5 relative; the CG iteration count and the line-search k exactly (trpo_inksci.py:146-158)."""
-    a, b = updates_8m["default"], updates_8m[variant]
-    sa, sb = a["stats"], b["stats"]
-    assert sa["cg_iters"] == sb["cg_iters"] == 10
-    assert sa["k"] == sb["k"] and sa["reverted"] == sb["reverted"]
+@pytest.fixture(scope="module")
+def truth_8m(big_batch, updates_8m, tmp_path_factory):
+    """The same update in float64 (oracle/chunked_f64.py: the reference graph by autograd, chunked over the
+    8M states, CG / line search in float64), in a child process on the GPU (tests/bign_truth.py)."""
+    d = tmp_path_factory.mktemp("bign")
+    np.save(d / "old.npy", big_batch["old"])
+    out = d / "truth.npz"
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run([sys.executable, os.path.join(here, "bign_truth.py"), str(d / "old.npy"), str(out)],
+                   check=True, timeout=900)
+    with np.load(out, allow_pickle=False) as t:
+        return {k: t[k] for k in t.files}
+
+
+@pytest.mark.parametrize("variant", ["default", "low_seg=0", "bf16x6"])
+def test_c4_8m_whole_update_vs_float64(gpu_available, updates_8m, truth_8m, variant):
+    """The bench's headline update at its full size (8M states: discount + standardise + pg + 10 CG + shs + line
+    search, trpo_inksci.py:102-158) against its float64 evaluation. `default` is the arithmetic the bench number
+    is measured on (f16x3 + one-product low segment).
+
+    Bar: the CG count, the line-search k and the revert decision exactly; g, stepdir, fullstep and theta_new
+    within max(1e-5, 2 x the float32 reference's own error) norm-relative and elementwise; shs / lm / the losses
+    after the step likewise. The float32 term is there because g is badly conditioned at this size: its layer-0/1
+    blocks are sums over 8M states of adv_n * s_n with mean-zero advantages, so every per-state rounding is
+    amplified by mean(s)/std(s), and the same graph evaluated in float32 (oracle/chunked_f64.py, as the
+    reference's TF session does) lands ~1e-5 from float64 on those blocks."""
+    a, t = updates_8m[variant], truth_8m
+    sa = a["stats"]
+    assert sa["cg_iters"] == int(t["f64_cg_iters"]) == 10
+    assert sa["k"] == int(t["f64_k"]) and bool(sa["reverted"]) == bool(t["f64_reverted"])
     for key in ("g", "stepdir", "fullstep", "theta"):
-        print(f"{variant} {key}: rel L2 {rel_l2(a[key], b[key]):.2e}")
-        assert_vec_close(a[key], b[key], REL, f"{key}: default vs {variant} at 8M")
-    assert sa["shs"] == pytest.approx(sb["shs"], rel=REL)
-    assert sa["lm"] == pytest.approx(sb["lm"], rel=REL)
-    for key in ("surr_after", "ent_after"):
-        assert sa[key] == pytest.approx(sb[key], rel=REL)
-    assert sa["kl_after"] == pytest.approx(sb["kl_after"], rel=REL, abs=1e-9)
+        ref, ref32 = t[f"f64_{key}"], t[f"f32_{key}"]
+        floor = rel_l2(ref32, ref)
+        bar = max(REL, 2.0 * floor)
+        print(f"{variant} {key}: rel L2 vs float64 {rel_l2(a[key], ref):.2e} (float32 reference {floor:.2e}, "
+              f"bar {bar:.1e})")
+        assert_vec_close(a[key], ref, bar, f"{key}: {variant} vs float64 at 8M")
+    for key in ("shs", "lm", "surr_after", "ent_after", "kl_after"):
+        ref, ref32 = float(t[f"f64_{key}"]), float(t[f"f32_{key}"])
+        bar = max(REL, 2.0 * abs(ref32 - ref) / abs(ref))
+        assert sa[key] == pytest.approx(ref, rel=bar, abs=1e-9 if key == "kl_after" else 0.0), key

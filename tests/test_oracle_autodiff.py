@@ -92,3 +92,48 @@ def test_standardize_population_std():
     y = O.standardize(x)
     assert abs(y.mean()) < 1e-15
     assert y.std() == pytest.approx(1.0 / (1.0 + 1e-8 / x.std()), rel=1e-12)
+
+
+@pytest.mark.parametrize("chunk", [97, 1000])
+def test_chunked_f64_graph_matches_oracle(chunk):
+    """oracle/chunked_f64.py (the float64 truth of the 8M-state GPU tests) against the numpy oracle: losses,
+    pg, FVP and a whole update, the batch cut into row chunks summed with 1/N_global; advantages from the
+    equal-path lfilter form against the oracle's segmented recurrence."""
+    from oracle.chunked_f64 import ChunkedGraph, advantages_equal_paths
+    spec = O.PolicySpec(11, [32, 16], 5)
+    n = 600
+    d = O.synthetic_batch(spec, n, seed=11, episode_len=200, steady_state=False, perturb=0.1)
+    adv = advantages_equal_paths(d["rewards"], 200)
+    np.testing.assert_allclose(adv, d["advant"], rtol=1e-12, atol=1e-12)
+    th = d["theta"].astype(np.float64)
+    G = ChunkedGraph(spec, d["X"], d["actions"], adv, d["old_dist"], chunk=chunk)
+    v = np.random.RandomState(12).standard_normal(spec.n_params)
+    assert rel_l2(G.fvp(th, v), O.fvp_undamped(th, d["X"], v, spec)) < 1e-13
+    assert rel_l2(G.pg(th), O.policy_grad(th, d["X"], d["actions"], adv, d["old_dist"], spec)) < 1e-13
+    np.testing.assert_allclose(G.losses(th), O.losses(th, d["X"], d["actions"], adv, d["old_dist"], spec),
+                               rtol=1e-12, atol=1e-15)
+    ref = O.trpo_update(th, O.Batch(d["X"], d["actions"], adv, d["old_dist"]), spec, residual_tol=0.0)
+    got = G.update(th, residual_tol=0.0)
+    assert got["k"] == ref.k and got["cg_iters"] == ref.cg_iters and got["reverted"] == ref.reverted
+    for key, r in (("g", ref.g), ("stepdir", ref.stepdir), ("fullstep", ref.fullstep), ("theta", ref.theta_new)):
+        assert rel_l2(got[key], r) < 1e-11, key
+    assert got["shs"] == pytest.approx(ref.shs, rel=1e-11)
+
+
+def test_chunked_float32_graph_near_oracle():
+    """The float32 mode of the chunked graph (the reference-arithmetic floor of the 8M tests) is the float64
+    graph to float32 rounding."""
+    import torch
+    from oracle.chunked_f64 import ChunkedGraph
+    spec = O.PolicySpec(11, [32, 16], 5)
+    d = O.synthetic_batch(spec, 600, seed=13)
+    th = d["theta"].astype(np.float64)
+    G32 = ChunkedGraph(spec, d["X"], d["actions"], d["advant"], d["old_dist"], chunk=128, dtype=torch.float32)
+    G64 = ChunkedGraph(spec, d["X"], d["actions"], d["advant"], d["old_dist"], chunk=128)
+    v = np.random.RandomState(14).standard_normal(spec.n_params)
+    assert G32.pg(th).dtype == np.float32
+    assert rel_l2(G32.pg(th), G64.pg(th)) < 1e-5
+    assert rel_l2(G32.fvp(th, v), G64.fvp(th, v)) < 1e-5
+    u32, u64 = G32.update(th, residual_tol=0.0), G64.update(th, residual_tol=0.0)
+    assert u32["stepdir"].dtype == np.float32 and u32["k"] == u64["k"]
+    assert rel_l2(u32["stepdir"], u64["stepdir"]) < 1e-4

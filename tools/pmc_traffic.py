@@ -24,7 +24,7 @@ import sys
 # plane count: 2 = the default f16 split)
 SPECS = {
     "fvp_rfwd_l0": ("rowgemm_pl_kernel<1, 1>", 1, 0),                       # X planes, kRHidden (plane.hip)
-    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 11, 2, 2, 2>", 1, 0),      # kRZ into the tail
+    "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 11, 2, 1, 2, 32>", 1, 0),  # kRZ into the tail (BK 32)
     "fvp_rbwdwg_l1": ("rbwd0_kernel<2>", 1, 0),                             # R-backward + X^T RD_0 (rbwd0.hip)
     "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
 }

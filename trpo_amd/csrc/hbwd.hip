@@ -7,9 +7,10 @@
 // write D_{L-2}'s scaled f16 hi plane (the fused R-backward's one-product D_1 V_1^T segment, rbwd0.hip)
 // with one power-of-two scale per 32-row tile, which replaces the separate split_planes pass over D_{L-2}.
 //
-// Layout: one thread per hidden column, a workgroup walks 32-row tiles (grid stride); the tile's head
-// deltas are staged in LDS and broadcast.  Sums run k = 0 .. A-1 as f32 fmaf chains (exact f32, as the
-// f32 MFMA row GEMM they replace; the order differs, the rounding level does not).
+// Layout: one thread per hidden column, a workgroup walks its split's 32-row tiles; the tile's head deltas
+// are staged in LDS and broadcast, and the next tile's H and deltas are loaded while the current one computes.
+// Sums run k = 0 .. A-1 as f32 fmaf chains (exact f32, as the f32 MFMA row GEMM they replace; the order
+// differs, the rounding level does not).
 #include "common.h"
 #include "kernels.h"
 
@@ -27,7 +28,8 @@ constexpr int kHbA = 32;        // max actions
 template <int AT>
 __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Args a) {
   __shared__ __attribute__((aligned(16))) float sd[2][kHbRows][AT];
-  __shared__ float sv[kHbRows][kHbThreads];   // the tile's D values, kept for the hi plane's tile scale
+  // the tile's H values (column c is thread c's own), then in place the D values kept for the hi plane's tile scale
+  __shared__ float sv[kHbRows][kHbThreads];
   __shared__ float sred[3][kHbThreads / 64];
   const int c = threadIdx.x, lane = c & 63, wv = c >> 6;
   const bool cv = c < a.Npad;
@@ -45,51 +47,68 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
   // workgroup s walks split s's rows (the weight-gradient slabs' partition, engine set_splits)
   const int r0 = blockIdx.x * a.rows_per_split;
   const int r1 = min(a.rows, r0 + a.rows_per_split);
+  // one tile ahead in registers: column c of the tile's 32 H rows, and this thread's share of the head deltas
+  // (2 x 32 x AT floats over 256 threads); they move to LDS at the top of the tile, so the next tile's loads
+  // are in flight during this tile's FMAs
+  constexpr int kSt = 2 * kHbRows * AT / kHbThreads;
+  float hc[kHbRows], pc[kSt];
+  auto load = [&](int t0, float (&hv)[kHbRows], float (&pv)[kSt]) {
+    const int nr = min(kHbRows, r1 - t0);
+#pragma unroll
+    for (int r = 0; r < kHbRows; ++r) hv[r] = (r < nr && cv) ? a.H[(size_t)(t0 + r) * a.Npad + c] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) {
+      const int i = c + u * kHbThreads;
+      const int m = i / (kHbRows * AT), r = (i / AT) % kHbRows, j = i % AT;
+      const float* src = m ? a.DS2 : a.D2;
+      pv[u] = (r < nr && j < a.A) ? src[(size_t)(t0 + r) * a.Apad + j] : 0.0f;
+    }
+  };
+  using cfloat = const __attribute__((address_space(4))) float;   // not written by this kernel
+  cfloat* d2c = (cfloat*)a.D2;
+  cfloat* ds2c = (cfloat*)a.DS2;
+  if (r0 < r1) load(r0, hc, pc);
   for (int t0 = r0; t0 < r1; t0 += kHbRows) {
     const int tile = t0 / kHbRows;
     const int nr = min(kHbRows, r1 - t0);
+    __syncthreads();   // the previous tile's deltas and values are consumed
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) (&sd[0][0][0])[c + u * kHbThreads] = pc[u];
+#pragma unroll
+    for (int r = 0; r < kHbRows; ++r) sv[r][c] = hc[r];
+    __syncthreads();
+    if (t0 + kHbRows < r1) load(t0 + kHbRows, hc, pc);   // in flight during this tile's FMAs
     // the tile's own weight-gradient partials, added to the split's sums once per tile: a split is ~15k rows
     // at C4, and one f32 running sum over all of them would carry ~sqrt(n) roundings
     float tw[AT];
 #pragma unroll
     for (int j = 0; j < AT; ++j) tw[j] = 0.0f;
     float tb = 0.0f;
-    __syncthreads();   // the previous tile's deltas and values are consumed
-    for (int i = c; i < 2 * kHbRows * AT; i += kHbThreads) {
-      const int m = i / (kHbRows * AT), r = (i / AT) % kHbRows, j = i % AT;
-      const float* src = m ? a.DS2 : a.D2;
-      sd[m][r][j] = (r < nr && j < a.A) ? src[(size_t)(t0 + r) * a.Apad + j] : 0.0f;
-    }
-    __syncthreads();
     float tm = 0.0f;
-#pragma unroll 4
-    for (int r = 0; r < kHbRows; ++r) {
+#pragma unroll 2
+    for (int r = 0; r < nr; ++r) {
       float d = 0.0f, s = 0.0f;
+      const float h = sv[r][c];
+      // the row's head deltas are the same for every thread: read them through the constant address space, so
+      // they arrive in SGPRs by scalar loads and feed the FMAs as scalar operands (LDS broadcasts of them cost
+      // 8 LDS cycles per 16 B and bound the kernel)
+      const size_t rb = (size_t)(t0 + r) * a.Apad;
+      // (rows are Apad = AT floats: unconditional loads merge into s_load_dwordx16; the padding columns are
+      // selected away, whatever they hold)
 #pragma unroll
-      for (int j = 0; j < AT; j += 4) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(&sd[0][r][j]);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(&sd[1][r][j]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          d = fmaf(x[q], w[j + q], d);
-          s = fmaf(y[q], w[j + q], s);
-        }
+      for (int j = 0; j < AT; ++j) {
+        const float xr = d2c[rb + j], yr = ds2c[rb + j];
+        const float x = j < a.A ? xr : 0.0f;
+        const float y = j < a.A ? yr : 0.0f;
+        d = fmaf(x, w[j], d);
+        s = fmaf(y, w[j], s);
+        if (wg) tw[j] = fmaf(h, y, tw[j]);
       }
-      float o1 = 0.0f;
+      const float om = (1.0f - h) * (1.0f + h);
+      const float o1 = d * om;
+      const float o2 = s * om;
       if (r < nr && cv) {
         const size_t idx = (size_t)(t0 + r) * a.Npad + c;
-        const float h = a.H[idx];
-        if (wg) {
-#pragma unroll
-          for (int j = 0; j < AT; j += 4) {
-            const f32x4 y = *reinterpret_cast<const f32x4*>(&sd[1][r][j]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tw[j + q] = fmaf(h, y[q], tw[j + q]);
-          }
-        }
-        const float om = (1.0f - h) * (1.0f + h);
-        o1 = d * om;
-        const float o2 = s * om;
         a.D1[idx] = o1;
         a.DS1[idx] = o2;
         mx1 = fmaxf(mx1, fabsf(o1));
@@ -97,7 +116,7 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
         tm = fmaxf(tm, fabsf(o1));
       }
       sv[r][c] = o1;
-      if (wg && c < a.A && r < nr) tb += sd[1][r][c];
+      if (wg && c < a.A) tb += sd[1][r][c];   // rows past the end were staged as 0
     }
     if (wg) {
 #pragma unroll
@@ -160,7 +179,7 @@ bool head_bwd2_eligible(int A, int Npad) { return A <= kHbA && Npad <= kHbThread
 
 void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s) {
   if (a.rows <= 0) return;
-  if (!head_bwd2_eligible(a.A, a.Npad) || a.Apad < a.A || !a.WB || !a.D2 || !a.DS2 || !a.H || !a.D1 || !a.DS1)
+  if (!head_bwd2_eligible(a.A, a.Npad) || a.Apad != (a.A + 3) / 4 * 4 || !a.WB || !a.D2 || !a.DS2 || !a.H || !a.D1 || !a.DS1)
     throw std::runtime_error("head_bwd2: unsupported shape or missing operand");
   if (a.D1h && (!a.eD1t || a.d1_mpad < a.rows || a.Npad % 32))
     throw std::runtime_error("head_bwd2: hi plane without its exponents or stride");
@@ -200,8 +219,9 @@ constexpr int kHfLd = kHfK + 1;
 template <int AT, bool PREP>
 __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) {
   __shared__ float sH[kHfRows * kHfLd];
-  __shared__ __attribute__((aligned(16))) float sW[kHfK][AT];
   __shared__ float sred[2][kHfRows / 64];
+  using cfloat = const __attribute__((address_space(4))) float;   // not written by this kernel
+  cfloat* wc = (cfloat*)a.W;
   const int t = threadIdx.x;
   const int nchunk = (a.K + kHfK - 1) / kHfK;
   float mD = 0.0f, mS = 0.0f;
@@ -229,20 +249,20 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) sH[r * kHfLd + col + e] = nx[q][e];
       }
-      for (int i = t; i < kHfK * AT; i += kHfRows) {
-        const int k = i / AT, j = i % AT, kk = kHfK * c + k;
-        sW[k][j] = (kk < a.K && j < a.A) ? a.W[(size_t)kk * a.Apad + j] : 0.0f;
-      }
       __syncthreads();
       if (c + 1 < nchunk) load_chunk(c + 1);
+      // W's row k is the same for every thread: scalar loads through the constant address space, FMAs with
+      // SGPR operands (an LDS broadcast of it costs 8 LDS cycles per 16 B and bound the kernel). Rows are
+      // Apad = AT floats; padding columns are selected away.
+      const int kn = min(kHfK, a.K - kHfK * c);
 #pragma unroll 8
-      for (int k = 0; k < kHfK; ++k) {
+      for (int k = 0; k < kn; ++k) {
         const float h = sH[t * kHfLd + k];
+        const size_t wb = (size_t)(kHfK * c + k) * AT;
 #pragma unroll
-        for (int j = 0; j < AT; j += 4) {
-          const f32x4 w4 = *reinterpret_cast<const f32x4*>(&sW[k][j]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[j + e] = fmaf(h, w4[e], acc[j + e]);
+        for (int j = 0; j < AT; ++j) {
+          const float wr = wc[wb + j];
+          acc[j] = fmaf(h, j < a.A ? wr : 0.0f, acc[j]);
         }
       }
     }
@@ -289,12 +309,14 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
       if constexpr (PREP) {
         // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps); surr logit delta
         // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead)
-        double B[AT], spB = 0.0, rest = 0.0;
+        // (B_j is recomputed in the output loop instead of held: a double array of AT entries cost 2 AT VGPRs
+        // and half the occupancy)
+        double spB = 0.0, rest = 0.0;
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
           const double pd = p[j];
-          B[j] = j < a.A ? (double)kEps / (pd + (double)kEps) : 0.0;
-          spB += pd * B[j];
+          const double Bj = j < a.A ? (double)kEps / (pd + (double)kEps) : 0.0;
+          spB += pd * Bj;
           rest += (j < a.A && j != av) ? pd : 0.0;
         }
         const double coef = -(double)adv * a.invN / (double)olda * (double)pa;
@@ -306,7 +328,8 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
           if (j < a.Apad) {
             const bool real = j < a.A;
             const double pd = p[j];
-            const float dl = real ? (float)(pd * a.invN * (B[j] - spB)) : 0.0f;
+            const double Bj = real ? (double)kEps / (pd + (double)kEps) : 0.0;
+            const float dl = real ? (float)(pd * a.invN * (Bj - spB)) : 0.0f;
             const float ds = real ? (float)(coef * (j == av ? rest : -pd)) : 0.0f;
             Pr[j] = real ? p[j] : 0.0f;
             Dr[j] = dl;
@@ -362,7 +385,7 @@ bool head_fwd_eligible(int A, int K) { return A <= 32 && K >= 1 && K <= 4096; }
 
 void launch_head_fwd(const HeadFwdArgs& a, int num_cus, hipStream_t s) {
   if (a.rows <= 0) return;
-  if (!head_fwd_eligible(a.A, a.K) || a.Apad < a.A || a.Kpad < a.K || a.Kpad % 4 || !a.H || !a.W || !a.bias ||
+  if (!head_fwd_eligible(a.A, a.K) || a.Apad != (a.A + 3) / 4 * 4 || a.Kpad < a.K || a.Kpad % 4 || !a.H || !a.W || !a.bias ||
       !a.old || !a.act || !a.adv || !a.rowterms || (a.prep && (!a.P || !a.D || !a.DS)))
     throw std::runtime_error("head_fwd: unsupported shape or missing operand");
   const int64_t tiles = (a.rows + kHfRows - 1) / kHfRows;
