@@ -189,8 +189,8 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
 
 /* ---- kernel-variant switches (for A/B measurements and variant parity tests) ----------
  * "split_mfma" (0 = f32 MFMA row GEMMs; 5 = the 256 x 256 split row-GEMM tile for outputs wider than
- * 128, at BK 32 on f16 planes, the default; 6 = the same tile at BK 16; any other value = 128 x 256), "split_wg" (0 = f32 weight gradients;
- * 1 = split tile for fan_out > 128), "chain" (fused FVP chain: 0 off, 1 auto, 2..4 forced variants),
+ * 128, at BK 32 on f16 planes, the default; 6 = the same tile at BK 16; any other value = 128 x 256),
+ * "split_wg" (0 = f32 weight gradients; 1 = split tile for fan_out > 128), "chain" (fused FVP chain: 0 off, 1 auto, 2..4 forced variants),
  * "split_f16" (split GEMMs on scaled f16 hi+lo planes), "split_min_k" (few-k row GEMMs stay on f32
  * MFMA), "graphs" (1 = trpo_update replays its sync-free prefix as a captured hipGraph, all-reduces
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
@@ -206,7 +206,13 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * "rbwd0" (1 = layer 1's R-backward and layer 0's weight gradient run as one launch of rbwd0.hip:
  * RD_0 stays in registers and X^T RD_0 is reduced from the engine's X planes; eligible on the f16
  * split with planes on, obs <= 128, hidden widths <= 256 and multiples of 32; also serves the policy
- * gradient's layer-1 backward; default 1).
+ * gradient's layer-1 backward; default 1),
+ * "hbwd2" (1 = the prepare pass's and the policy gradient's backward through the softmax head's layer
+ * run as one launch of hbwd.hip over one read of H_{L-1}, which also writes D_{L-2}'s f16 hi plane for
+ * rbwd0 and the policy gradient's head-layer weight gradient; f32 FMA; <= 32 actions, last hidden
+ * width <= 256; default 1), "head_fwd" (softmax head forwards with one state per lane on f32 FMAs,
+ * hbwd.hip: 1 = the prepare and the line-search heads, 2 = the line-search heads only, the default;
+ * 0 = off).
  * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed
  * from the build in round 4; tools/patches/pruned_variants.patch restores them.
  * Process-wide. */

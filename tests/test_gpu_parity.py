@@ -283,7 +283,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
     {"hbwd2": 0}, {"hbwd2": 0, "chain": 0},                   # separate head backwards (prepare / policy gradient)
-    {"head_fwd": 0}, {"head_fwd": 0, "chain": 0},             # the f32 MFMA row GEMM's 32-lane softmax head
+    {"head_fwd": 0}, {"head_fwd": 1}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and

@@ -789,8 +789,10 @@ struct trpo_engine {
       a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
       a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
       if (l == 0 && planes_l0()) attach_x_planes(a.seg[0], wf3[0], W0b);
-      if (l == L - 1 && g_options.head_fwd != 0 && head_fwd_eligible(w[L], w[L - 1]) &&
-          (head == RowEpi::kPrepHead || head == RowEpi::kLossHead)) {
+      // head_fwd 1: the prepare and the loss heads; 2: the loss heads only
+      const int hfo = g_options.head_fwd;
+      if (l == L - 1 && (hfo == 1 || hfo == 2) && head_fwd_eligible(w[L], w[L - 1]) &&
+          ((head == RowEpi::kPrepHead && hfo == 1) || head == RowEpi::kLossHead)) {
         // the softmax head with one state per lane (hbwd.hip): bound by its read of H_{L-1}
         HeadFwdArgs hf{};
         hf.rows = n;

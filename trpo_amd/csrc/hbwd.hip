@@ -24,6 +24,10 @@ constexpr int kHbRows = 32;     // rows per tile
 constexpr int kHbThreads = 256; // one hidden column per thread (Npad <= 256)
 constexpr int kHbA = 32;        // max actions
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // AT: actions rounded up to a multiple of 4 (the register image of W^T's column)
 template <int AT>
 __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Args a) {
@@ -64,9 +68,6 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
       pv[u] = (r < nr && j < a.A) ? src[(size_t)(t0 + r) * a.Apad + j] : 0.0f;
     }
   };
-  using cfloat = const __attribute__((address_space(4))) float;   // not written by this kernel
-  cfloat* d2c = (cfloat*)a.D2;
-  cfloat* ds2c = (cfloat*)a.DS2;
   if (r0 < r1) load(r0, hc, pc);
   for (int t0 = r0; t0 < r1; t0 += kHbRows) {
     const int tile = t0 / kHbRows;
@@ -86,23 +87,19 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
     float tb = 0.0f;
     float tm = 0.0f;
 #pragma unroll 2
-    for (int r = 0; r < nr; ++r) {
+    for (int r = 0; r < kHbRows; ++r) {
       float d = 0.0f, s = 0.0f;
       const float h = sv[r][c];
-      // the row's head deltas are the same for every thread: read them through the constant address space, so
-      // they arrive in SGPRs by scalar loads and feed the FMAs as scalar operands (LDS broadcasts of them cost
-      // 8 LDS cycles per 16 B and bound the kernel)
-      const size_t rb = (size_t)(t0 + r) * a.Apad;
-      // (rows are Apad = AT floats: unconditional loads merge into s_load_dwordx16; the padding columns are
-      // selected away, whatever they hold)
 #pragma unroll
-      for (int j = 0; j < AT; ++j) {
-        const float xr = d2c[rb + j], yr = ds2c[rb + j];
-        const float x = j < a.A ? xr : 0.0f;
-        const float y = j < a.A ? yr : 0.0f;
-        d = fmaf(x, w[j], d);
-        s = fmaf(y, w[j], s);
-        if (wg) tw[j] = fmaf(h, y, tw[j]);
+      for (int j = 0; j < AT; j += 4) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&sd[0][r][j]);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(&sd[1][r][j]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          d = fmaf(x[q], w[j + q], d);
+          s = fmaf(y[q], w[j + q], s);
+          if (wg) tw[j + q] = fmaf(h, y[q], tw[j + q]);   // rows past the end have h = 0
+        }
       }
       const float om = (1.0f - h) * (1.0f + h);
       const float o1 = d * om;
@@ -217,11 +214,10 @@ constexpr int kHfK = 32;       // columns of H per chunk
 constexpr int kHfLd = kHfK + 1;
 
 template <int AT, bool PREP>
-__global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) {
+__global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28 ? 4 : 3)) head_fwd_kernel(const HeadFwdArgs a) {
   __shared__ float sH[kHfRows * kHfLd];
+  __shared__ __attribute__((aligned(16))) float sW[kHfK][AT];
   __shared__ float sred[2][kHfRows / 64];
-  using cfloat = const __attribute__((address_space(4))) float;   // not written by this kernel
-  cfloat* wc = (cfloat*)a.W;
   const int t = threadIdx.x;
   const int nchunk = (a.K + kHfK - 1) / kHfK;
   float mD = 0.0f, mS = 0.0f;
@@ -237,9 +233,9 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
                                          : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
     };
-    float acc[AT];
+    f32x2 acc2[AT / 2];   // output pairs: one packed FMA per pair
 #pragma unroll
-    for (int j = 0; j < AT; ++j) acc[j] = 0.0f;
+    for (int j = 0; j < AT / 2; ++j) acc2[j] = f32x2{0.0f, 0.0f};
     load_chunk(0);
     for (int c = 0; c < nchunk; ++c) {
       __syncthreads();   // the previous chunk's reads are done
@@ -249,20 +245,20 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) sH[r * kHfLd + col + e] = nx[q][e];
       }
+      for (int i = t; i < kHfK * AT; i += kHfRows) {
+        const int k = i / AT, j = i % AT, kk = kHfK * c + k;
+        sW[k][j] = (kk < a.K && j < a.A) ? a.W[(size_t)kk * a.Apad + j] : 0.0f;
+      }
       __syncthreads();
       if (c + 1 < nchunk) load_chunk(c + 1);
-      // W's row k is the same for every thread: scalar loads through the constant address space, FMAs with
-      // SGPR operands (an LDS broadcast of it costs 8 LDS cycles per 16 B and bound the kernel). Rows are
-      // Apad = AT floats; padding columns are selected away.
-      const int kn = min(kHfK, a.K - kHfK * c);
 #pragma unroll 8
-      for (int k = 0; k < kn; ++k) {
+      for (int k = 0; k < kHfK; ++k) {
         const float h = sH[t * kHfLd + k];
-        const size_t wb = (size_t)(kHfK * c + k) * AT;
 #pragma unroll
-        for (int j = 0; j < AT; ++j) {
-          const float wr = wc[wb + j];
-          acc[j] = fmaf(h, j < a.A ? wr : 0.0f, acc[j]);
+        for (int j = 0; j < AT; j += 4) {
+          const f32x4 w4 = *reinterpret_cast<const f32x4*>(&sW[k][j]);
+          acc2[j / 2] = pk_fma(f32x2{h, h}, f32x2{w4[0], w4[1]}, acc2[j / 2]);
+          acc2[j / 2 + 1] = pk_fma(f32x2{h, h}, f32x2{w4[2], w4[3]}, acc2[j / 2 + 1]);
         }
       }
     }
@@ -273,7 +269,7 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
       float zm = -INFINITY;
 #pragma unroll
       for (int j = 0; j < AT; ++j) {
-        z[j] = j < a.A ? acc[j] + a.bias[j] : -INFINITY;
+        z[j] = j < a.A ? acc2[j / 2][j % 2] + a.bias[j] : -INFINITY;
         zm = fmaxf(zm, z[j]);
       }
       float es = 0.0f;
@@ -309,8 +305,7 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
       if constexpr (PREP) {
         // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps); surr logit delta
         // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead)
-        // (B_j is recomputed in the output loop instead of held: a double array of AT entries cost 2 AT VGPRs
-        // and half the occupancy)
+        // (B_j is recomputed in the output loop instead of held: a double array of AT entries costs 2 AT VGPRs)
         double spB = 0.0, rest = 0.0;
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
@@ -327,7 +322,8 @@ __global__ void __launch_bounds__(kHfRows) head_fwd_kernel(const HeadFwdArgs a) 
         for (int j = 0; j < AT; ++j) {
           if (j < a.Apad) {
             const bool real = j < a.A;
-            const double pd = p[j];
+            double pd = p[j];
+            asm volatile("" : "+v"(pd));   // recomputed, not kept from the first loop (CSE would hold AT doubles)
             const double Bj = real ? (double)kEps / (pd + (double)kEps) : 0.0;
             const float dl = real ? (float)(pd * a.invN * (Bj - spB)) : 0.0f;
             const float ds = real ? (float)(coef * (j == av ? rest : -pd)) : 0.0f;

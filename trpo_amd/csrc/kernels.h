@@ -30,7 +30,8 @@ struct Options {
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
   int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
                    // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
-  int head_fwd;    // engine: the softmax head forward (prepare and line search) with one state per lane on f32 FMAs
+  int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (1 prepare + line search, 2 line
+                   // search only)
                    // (hbwd.hip) instead of the f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 on
 };
 
