@@ -17,7 +17,8 @@ n_global = 8M scaling through a row slice the oracle does evaluate:
 * whole update  the bench's full update at 8M (discount, standardise, pg, 10 CG, shs, line search) on its
                 own arithmetic (f16x3 + one-product low segment), on three products everywhere and on the
                 exact bf16x6 split, against the same update in float64 (oracle/chunked_f64.py in a child
-                process): CG count and k exact, vectors at max(1e-5, 2 x float32's own error)
+                process): CG count and k exact; the default's vectors at 1e-5, the others at
+                max(1e-5, 2 x float32's own error)
 """
 import os
 import subprocess
@@ -172,12 +173,12 @@ def test_c4_8m_whole_update_vs_float64(gpu_available, updates_8m, truth_8m, vari
     search, trpo_inksci.py:102-158) against its float64 evaluation. `default` is the arithmetic the bench number
     is measured on (f16x3 + one-product low segment).
 
-    Bar: the CG count, the line-search k and the revert decision exactly; g, stepdir, fullstep and theta_new
-    within max(1e-5, 2 x the float32 reference's own error) norm-relative and elementwise; shs / lm / the losses
-    after the step likewise. The float32 term is there because g is badly conditioned at this size: its layer-0/1
-    blocks are sums over 8M states of adv_n * s_n with mean-zero advantages, so every per-state rounding is
-    amplified by mean(s)/std(s), and the same graph evaluated in float32 (oracle/chunked_f64.py, as the
-    reference's TF session does) lands ~1e-5 from float64 on those blocks."""
+    Bar: the CG count, the line-search k and the revert decision exactly. For `default`, g, stepdir, fullstep
+    and theta_new within 1e-5 of float64, norm-relative and elementwise, and shs / lm / the losses after the step
+    within 1e-5 relative. The other two arithmetics get max(1e-5, 2 x the float32 reference's own error): g is
+    badly conditioned at this size (sums over 8M states of adv_n * s_n with mean-zero advantages), and the
+    same graph evaluated in float32 (oracle/chunked_f64.py, as the reference's TF session does) lands 8e-6 / 1.4e-5
+    from float64 on g / stepdir."""
     a, t = updates_8m[variant], truth_8m
     sa = a["stats"]
     assert sa["cg_iters"] == int(t["f64_cg_iters"]) == 10
@@ -185,11 +186,11 @@ def test_c4_8m_whole_update_vs_float64(gpu_available, updates_8m, truth_8m, vari
     for key in ("g", "stepdir", "fullstep", "theta"):
         ref, ref32 = t[f"f64_{key}"], t[f"f32_{key}"]
         floor = rel_l2(ref32, ref)
-        bar = max(REL, 2.0 * floor)
+        bar = REL if variant == "default" else max(REL, 2.0 * floor)
         print(f"{variant} {key}: rel L2 vs float64 {rel_l2(a[key], ref):.2e} (float32 reference {floor:.2e}, "
               f"bar {bar:.1e})")
         assert_vec_close(a[key], ref, bar, f"{key}: {variant} vs float64 at 8M")
     for key in ("shs", "lm", "surr_after", "ent_after", "kl_after"):
         ref, ref32 = float(t[f"f64_{key}"]), float(t[f"f32_{key}"])
-        bar = max(REL, 2.0 * abs(ref32 - ref) / abs(ref))
+        bar = REL if variant == "default" else max(REL, 2.0 * abs(ref32 - ref) / abs(ref))
         assert sa[key] == pytest.approx(ref, rel=bar, abs=1e-9 if key == "kl_after" else 0.0), key

@@ -284,6 +284,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
     {"hbwd2": 0}, {"hbwd2": 0, "chain": 0},                   # separate head backwards (prepare / policy gradient)
     {"head_fwd": 0}, {"head_fwd": 1}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
+    {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -291,7 +292,8 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
-                                           "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd")}
+                                           "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
+                                           "splits", "pg_splits")}
     try:
         for k, v in opts.items():
             set_option(k, v)

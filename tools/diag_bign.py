@@ -51,6 +51,16 @@ def main():
         n = int(np.prod(shape))
         bounds.append((f"{'W' if len(shape) == 2 else 'b'}{len(bounds) // 2}", off, off + n))
         off += n
+    G32 = ChunkedGraph(SPEC, X, actions, advantages_equal_paths(rewards, 200), old, device="cuda", chunk=1 << 20,
+                       dtype=torch.float32)
+    g32 = G32.update(theta, residual_tol=0.0)
+    del G32
+    torch.cuda.empty_cache()
+    for k in ("g", "stepdir"):
+        print(f"   {k} per block vs f64: " + " ".join(f"{nm} {rel(g32[k][a:b], truth[k][a:b]):.1e}"
+                                                  for nm, a, b in bounds), flush=True)
+    print("torch float32 graph | vs f64: " + " ".join(f"{k} {rel(g32[k], truth[k]):.2e}" for k in ("g", "stepdir", "theta")),
+          flush=True)
 
     def run(opts):
         saved = {k: get_option(k) for k in opts}
@@ -71,10 +81,11 @@ def main():
 
     sets = {
         "f32": {"split_mfma": 0, "split_wg": 0, "hbwd2": 0, "head_fwd": 0},
-        "bf16x6": {"split_f16": 0},
         "default": {},
-        "hbwd2=0": {"hbwd2": 0},
-
+        "pg_splits=512": {"pg_splits": 512},
+        "splits=2048": {"splits": 2048},
+        "bf16x6": {"split_f16": 0},
+        "low_seg=0": {"low_seg": 0},
     }
     res = {}
     for name, opts in sets.items():

@@ -77,6 +77,7 @@ struct trpo_engine {
   double* rowterms = nullptr;
   float* slab = nullptr;
   int S = 1, rows_per_split = 16;
+  int S_pg = 1, S_cur = 1;
   int64_t slab_stride = 0;
   double *partA = nullptr, *partB = nullptr, *part3 = nullptr, *local3 = nullptr, *dscal = nullptr;
   void* scan_ws = nullptr;
@@ -371,8 +372,16 @@ struct trpo_engine {
     // the activations at HBM rate; small policies take up to 2048 splits while the slabs fit 128 MB
     if (tiles_max == 1)
       s_target = (int)std::max<int64_t>(s_target, std::min<int64_t>(2048, (int64_t(128) << 20) / (slab_stride * 4)));
-    slab = dalloc<float>((size_t)s_target * slab_stride);
+    if (g_options.splits > 0) s_target = std::min(g_options.splits, 8192);
+    // the policy gradient (once per update) takes 4x the splits, up to 2048: its layer-0/1 blocks are sums of
+    // adv_n s_n over the batch with mean-zero advantages, whose f32 MFMA accumulation error grows with the rows
+    // per split (numerics at 8M); the FVPs keep the faster geometry
+    int s_pg = std::max(s_target, std::min(2048, 4 * s_target));
+    if (g_options.pg_splits > 0) s_pg = std::min(g_options.pg_splits, 8192);
+    slab = dalloc<float>((size_t)std::max(s_target, s_pg) * slab_stride);
     S = s_target;
+    S_pg = s_pg;
+    S_cur = S;
     partA = dalloc<double>(kRedBlocks * 3);
     partB = dalloc<double>(kRedBlocks * 3);
     part3 = dalloc<double>(kRedBlocks * 3);
@@ -594,9 +603,15 @@ struct trpo_engine {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
+  // the split geometry of the launches that follow: S (FVP weight gradients) or S_pg (policy gradient)
+  void use_splits(int s) {
+    if (s == S_cur) return;
+    S_cur = s;
+    set_splits();
+  }
   void set_splits() {
     // rows per split: a multiple of the 16-row k-tile, >= 64 rows
-    const int smax = S;
+    const int smax = S_cur;
     int64_t rps = (n + smax - 1) / smax;
     rps = std::max<int64_t>(64, (rps + 31) / 32 * 32);   // multiple of the largest wgrad k-tile
     rows_per_split = (int)rps;
@@ -918,6 +933,7 @@ struct trpo_engine {
         hb.DS1 = RD[L - 2];
         hb.am_d1 = am_d(L - 2);
         hb.am_ds1 = am_ds(L - 2);
+        use_splits(S_pg);   // the slab block it writes is reduced with the policy gradient's
         hb.splits = active_splits;
         hb.rows_per_split = rows_per_split;
         hb.slab = slab;   // the policy gradient's W_{L-1} / b_{L-1} block, reduced by policy_grad()
@@ -933,6 +949,7 @@ struct trpo_engine {
         Scope sp(this, "bwd2_l2");
         launch_head_bwd2(hb, num_cus, stream);
         check_launch();
+        use_splits(S);
         ds_ready = true;
         if (hb.D1h) {
           d1_plane = true;
@@ -1009,6 +1026,7 @@ struct trpo_engine {
   void policy_grad() {
     prepare();
     ensure_w3();
+    use_splits(S_pg);
     // surr backward: DS_{l-1} = (DS_l W_l^T)(1-H_l^2) ; DS of hidden layers lives in RD scratch
     std::vector<float*> DS(L);
     DS[L - 1] = DSL;
@@ -1053,6 +1071,7 @@ struct trpo_engine {
                   nullptr, t);
     }
     reduce_grad(g, nullptr);
+    use_splits(S);
   }
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
@@ -2404,6 +2423,8 @@ static int* option_slot(const std::string& k) {
   if (k == "rbwd0") return &g_options.rbwd0;
   if (k == "hbwd2") return &g_options.hbwd2;
   if (k == "head_fwd") return &g_options.head_fwd;
+  if (k == "splits") return &g_options.splits;
+  if (k == "pg_splits") return &g_options.pg_splits;
   throw ArgError("unknown option " + k);
 }
 
