@@ -804,10 +804,12 @@ struct trpo_engine {
       a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
       a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
       if (l == 0 && planes_l0()) attach_x_planes(a.seg[0], wf3[0], W0b);
-      // head_fwd 1: the prepare and the loss heads; 2: the loss heads only
+      // head_fwd 1: the prepare and the loss heads; 2: the loss heads, and the prepare head for <= 8 actions (its
+      // row epilogue is cheap there; at 18 actions the row GEMM's 32-lane head is faster: DESIGN.md §4)
       const int hfo = g_options.head_fwd;
+      const bool prep_hf = hfo == 1 || (hfo == 2 && w[L] <= 8);
       if (l == L - 1 && (hfo == 1 || hfo == 2) && head_fwd_eligible(w[L], w[L - 1]) &&
-          ((head == RowEpi::kPrepHead && hfo == 1) || head == RowEpi::kLossHead)) {
+          ((head == RowEpi::kPrepHead && prep_hf) || head == RowEpi::kLossHead)) {
         // the softmax head with one state per lane (hbwd.hip): bound by its read of H_{L-1}
         HeadFwdArgs hf{};
         hf.rows = n;
@@ -1522,7 +1524,7 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready;
+    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready, d1_plane, d1_tiled;
   } upd_flags{};
   void drop_graph() {
     if (upd_exec) {
@@ -1551,6 +1553,8 @@ struct trpo_engine {
       have_returns = upd_flags.have_returns;
       prep_e_top = upd_flags.prep_e_top;
       ds_ready = upd_flags.ds_ready;
+      d1_plane = upd_flags.d1_plane;
+      d1_tiled = upd_flags.d1_tiled;
       return;
     }
     if (!same) {
@@ -1585,7 +1589,8 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready};
+    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready, d1_plane,
+                            d1_tiled};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;

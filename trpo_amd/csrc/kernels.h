@@ -31,7 +31,7 @@ struct Options {
   int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
                    // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
   int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (1 prepare + line search, 2 line
-                   // search only)
+                   // search, and the prepare head when the head has <= 8 actions)
   int splits;      // engine: weight-gradient split-K slabs of the FVP launches (0 = auto: 512 at C4)
   int pg_splits;   // engine: the policy gradient's split-K slabs (0 = auto: 4 x splits, at most 2048)
                    // (hbwd.hip) instead of the f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 on
