@@ -184,3 +184,27 @@ def test_learn_nan_entropy_exit(gpu_available):
     agent.engine.update = update
     hist = agent.learn(max_iterations=10, n_envs=1, seed=3, log=None)
     assert len(hist) == 2 and hist[-1].get("nan_exit") and np.isnan(hist[-1]["entropy"])
+
+
+def test_learn_two_ranks_share_gpu(gpu_available):
+    """learn() as two ranks on one GPU (TRPOAgent.set_ranks with the host transport): each rank rolls out
+    half of the timestep budget with its own draws; after every iteration both ranks hold bitwise-identical
+    policy and VF parameters, the episode count and mean reward are the concatenated rollouts', and
+    iteration 0's update equals one engine's update of the concatenated rollouts at 1e-5
+    (tools/mrank_learn.py; trpo_inksci.py:89-158)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tools", "mrank_learn.py"),
+           "--host-allreduce", "--iters", "3"]
+    res = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
+    assert "MRANK LEARN OK" in res.stdout
+    print(res.stdout.strip().splitlines()[-2])

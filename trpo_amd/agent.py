@@ -104,6 +104,48 @@ class TRPOAgent:
         self.train = True                                        # :28
         self.end_count = 0                                       # :29
         self.vf = VF(self.session, max_rows=max_rows, device=device)   # :73
+        self.rank, self.world, self.group = 0, 1, None
+
+    def set_ranks(self, rank: int, world: int, group=None, host_allreduce: bool = False):
+        """Run learn() as one of `world` ranks (one process per GPU, torch.distributed initialised by the
+        caller; `group` a gloo group for the host-side scalars, None = the default group, which must then
+        be gloo). Each rank rolls out its own share of the episode budget; the update's partial sums,
+        the advantage standardisation, the explained variance and the VF gradient are summed over the
+        ranks (the engine's and the VF's RCCL communicators, or with host_allreduce the stream-ordered
+        host transport over gloo, for ranks that share a GPU). Policy and VF parameters start identical
+        on every rank and stay so: every rank applies the same all-reduced step."""
+        self.rank, self.world, self.group = int(rank), int(world), group
+        if self.world <= 1:
+            return
+        import torch
+        import torch.distributed as dist
+        from .dist import broadcast_unique_id, init_engine_comm
+
+        def ar(arr):
+            dist.all_reduce(torch.from_numpy(arr), group=group)
+
+        if host_allreduce:
+            self.engine.comm_set_host_allreduce(ar, self.rank, self.world)
+        else:
+            init_engine_comm(self.engine, self.rank, self.world, group)
+
+        def vf_comm(net):   # the VF net is created at its first fit (utils.py:83)
+            if host_allreduce:
+                net.comm_set_host_allreduce(ar, self.rank, self.world)
+            else:
+                net.comm_init(broadcast_unique_id(Engine.comm_unique_id, self.rank, group), self.rank, self.world)
+
+        self.vf.on_create = vf_comm
+
+    def _host_sum(self, *vals: float) -> np.ndarray:
+        """Sum of host scalars over the ranks (gloo), float64; identity for one rank."""
+        a = np.array(vals, np.float64)
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            t = torch.from_numpy(a)
+            dist.all_reduce(t, group=self.group)
+        return a
 
     def feed(self, paths_or_batch, n_global: Optional[int] = None):
         """The feed dict of trpo_inksci.py:119-122 (+ rewards for :102-117)."""
@@ -161,8 +203,10 @@ class TRPOAgent:
         Returns one stats dict per iteration."""
         cfg = self.config
         eng = self.engine
+        # this rank's share of the timestep budget (trpo_inksci.py:96-100 over `world` ranks)
+        n_timesteps = -(-cfg["episodes_per_roll"] // self.world)
         # worst case rows of one rollout: every environment overshoots its budget by one episode
-        budget = -(-cfg["episodes_per_roll"] // n_envs)
+        budget = -(-n_timesteps // n_envs)
         worst = n_envs * (budget + min(cfg["max_steps"], 200) - 1)
         if worst > eng.max_rows:
             raise ValueError(f"learn(): a rollout of {n_envs} environments can reach {worst} steps, more than "
@@ -178,10 +222,12 @@ class TRPOAgent:
             if draws is not None:
                 ru, au, me = draws(i)
                 inj = {"reset_uniforms": ru, "action_uniforms": au, "max_episodes_per_env": me}
-            n, n_paths = eng.rollout_cartpole(n_envs=n_envs, n_timesteps=cfg["episodes_per_roll"],
-                                              max_pathlength=cfg["max_steps"], seed=seed * 1000003 + i,
+            n, n_paths = eng.rollout_cartpole(n_envs=n_envs, n_timesteps=n_timesteps,
+                                              max_pathlength=cfg["max_steps"],
+                                              seed=seed * 1000003 + i + 7919 * self.rank,
                                               train=self.train, **inj)                   # :96-100
-            eng.rollout_to_batch()                                                       # :108-122
+            n_global = int(self._host_sum(n)[0])
+            eng.rollout_to_batch(n_global=n_global)                                      # :108-122
             have_base = self.vf.predict_engine(eng)                                      # :103
             if record:
                 rb = self.vf.net.predict(np.empty(n, np.float64)) if have_base else np.zeros(n)
@@ -191,16 +237,19 @@ class TRPOAgent:
                 eng.compute_advantages_device(cfg["gamma"])                              # :104-117
             ep = eng.rollout_fetch_stats()
             episoderewards = np.add.reduceat(ep["rewards"], np.flatnonzero(ep["starts"]))   # :131
+            # the mean over every rank's episodes (one rank: episoderewards.mean())
+            ep_sum, ep_cnt = self._host_sum(episoderewards.sum(), len(episoderewards))
+            reward_mean = ep_sum / ep_cnt if self.world > 1 else float(episoderewards.mean())
             say("\n********** Iteration %i ************" % i)
             rec = {"iteration": i, "steps": n, "paths": n_paths, "train": self.train,
-                   "reward_mean": float(episoderewards.mean()), "end_count": self.end_count}
+                   "reward_mean": float(reward_mean), "end_count": self.end_count}
             if record:
                 rec.update({"rollout": eng.rollout_fetch(), "baseline": rb, "returns": r_ret, "advantages": r_adv})
-            if episoderewards.mean() > 1.1 * 500:                                        # :135-136
+            if reward_mean > 1.1 * 500:                                                  # :135-136
                 self.train = False
             rec["train"] = self.train                    # whether this iteration updates the policy
             if not self.train:                                                           # :137-141
-                say("Episode mean: %f" % episoderewards.mean())
+                say("Episode mean: %f" % reward_mean)
                 self.end_count += 1
                 rec["end_count"] = self.end_count
                 if self.end_count > 100:
@@ -208,13 +257,18 @@ class TRPOAgent:
                     break
             if self.train:
                 self.vf.fit_engine(eng)                                                  # :143
+                if record:
+                    rec["theta_before"] = eng.get_flat().copy()
                 st = eng.update(UpdateParams(cg_iters=10, residual_tol=1e-10, cg_damping=cfg["cg_damping"],
                                              max_kl=cfg["max_kl"], compute_advantages=False))     # :144-158
-                numeptotal += len(episoderewards)
+                if record:
+                    rec["theta"] = eng.get_flat().copy()
+                    rec["vf_params"] = self.vf.net.get_params().copy()
+                numeptotal += int(ep_cnt)
                 exp = eng.explained_variance()                                           # :167
                 stats = {
                     "Total number of episodes": numeptotal,
-                    "Average sum of rewards per episode": episoderewards.mean(),
+                    "Average sum of rewards per episode": reward_mean,
                     "Entropy": st["ent_after"],
                     "Baseline explained": exp,
                     "Time elapsed": "%.2f mins" % ((time.time() - start_time) / 60.0),

@@ -204,6 +204,7 @@ class VFNet:
 class VF(object):
     """utils.py:48-92 on the GPU."""
     coeffs = None
+    on_create = None   # callable(VFNet) run when the net is created
 
     def __init__(self, session, max_rows: Optional[int] = None, device: Optional[int] = None,
                  rng: Optional[np.random.RandomState] = None):
@@ -220,6 +221,8 @@ class VF(object):
         self.net = VFNet(int(shape), self.max_rows, (64, 64), self.device)
         self.net.set_params(vf_xavier_params(int(shape), (64, 64), self.rng))
         self.net.reset_optimizer()
+        if self.on_create is not None:   # multi-rank learn(): the net's gradient all-reduce (TRPOAgent.set_ranks)
+            self.on_create(self.net)
         reinit = getattr(self.session, "initialize_all_variables", None)
         if callable(reinit):
             reinit()
