@@ -808,13 +808,16 @@ def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
     (128, [256, 256], 18, 40037),      # several splits
     (37, [192, 200], 17, 2500),        # K = 200 for the fused R-backward, 17 actions
     (64, [256, 256, 256], 32, 900),    # depth 3: D_2 / DS_2 (no hi plane), A = 32
-], ids=["c4_dims", "many_splits", "odd", "depth3"])
+    (128, [256, 256], 18, -3001),      # C4 dims with tail = 0: the per-layer FVP reads E_1, written here as well
+], ids=["c4_dims", "many_splits", "odd", "depth3", "c4_dims_e1"])
 def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
     """hbwd.hip: the prepare pass's D_{L-2} and the policy gradient's DS_{L-2} in one read of H (and D_1's f16 hi
-    plane scaled per 32-row tile) against the two row-GEMM backwards (option hbwd2 = 0) and the float64 oracle:
-    g, Hv and a whole update (trpo_inksci.py:54,56-70,144-158)."""
+    plane scaled per 32-row tile, or E_{L-2} where the fused FVP reads it) against the two row-GEMM backwards
+    (option hbwd2 = 0) and the float64 oracle: g, Hv and a whole update (trpo_inksci.py:54,56-70,144-158)."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
+    no_tail = n < 0                       # negative n: the same rows with the fused tail off
+    n = abs(n)
     spec = O.PolicySpec(obs, hidden, A)
     dd = O.synthetic_batch(spec, n, seed=n + 5)
     th = dd["theta"].astype(np.float64)
@@ -823,6 +826,9 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
     gref = O.policy_grad(th, dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
     r = O.trpo_update(th, O.Batch(dd["X"], dd["actions"], dd["advant"], dd["old_dist"]), spec, np.float64, 10, 0.0)
     saved = get_option("hbwd2")
+    saved_tail = get_option("tail")
+    if no_tail:
+        set_option("tail", 0)
     out = {}
     try:
         for mode in (1, 0):
@@ -838,6 +844,7 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
             e.close()
     finally:
         set_option("hbwd2", saved)
+        set_option("tail", saved_tail)
     for mode in (1, 0):
         g, hv, g2, st, theta = out[mode]
         assert_vec_close(g, gref, REL, f"g hbwd2={mode}")

@@ -122,8 +122,10 @@ struct trpo_engine {
   // writes RD clears it
   bool ds_ready = false;
   bool use_hbwd2() const {
-    // the head layer's backward is the D-only (kPgBwd) step: a hidden layer below it, E_{L-2} not read
-    return g_options.hbwd2 != 0 && L >= 3 && head_bwd2_eligible(w[L], wp[L - 1]) && !e_top_needed();
+    // a hidden layer below the head layer, wider than 128 (one thread per column: at 64 columns three
+    // quarters of its lanes idle, and C3 ran 3 % slower than on the row GEMMs); E_{L-2} is written too
+    // where the FVP path reads it (no fused tail)
+    return g_options.hbwd2 != 0 && L >= 3 && wp[L - 1] > 128 && head_bwd2_eligible(w[L], wp[L - 1]);
   }
   int x_mpad = 0, x_ldp = 0;
   bool x_planes = false;   // Xh/Xl hold the current X
@@ -933,6 +935,7 @@ struct trpo_engine {
         hb.H = H[L - 1];
         hb.D1 = D[L - 2];
         hb.DS1 = RD[L - 2];
+        hb.E1 = prep_e_top ? E[L - 2] : nullptr;
         hb.am_d1 = am_d(L - 2);
         hb.am_ds1 = am_ds(L - 2);
         use_splits(S_pg);   // the slab block it writes is reduced with the policy gradient's

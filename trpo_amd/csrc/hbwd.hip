@@ -108,6 +108,7 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
         const size_t idx = (size_t)(t0 + r) * a.Npad + c;
         a.D1[idx] = o1;
         a.DS1[idx] = o2;
+        if (a.E1) a.E1[idx] = -2.0f * d * h;
         mx1 = fmaxf(mx1, fabsf(o1));
         mx2 = fmaxf(mx2, fabsf(o2));
         tm = fmaxf(tm, fabsf(o1));

@@ -478,6 +478,7 @@ struct HeadBwd2Args {
   uint16_t* D1h = nullptr;
   int d1_mpad = 0;
   int* eD1t = nullptr;
+  float* E1 = nullptr;       // E_{L-2} = -2 (D_{L-1} W^T) H (the kPrepBwd epilogue's second output), when read
   // workgroup s takes the rows of split s (the weight-gradient slab partition); slab != NULL: it also writes the
   // policy gradient's last-layer weight gradient (H^T DS2, W block [N][A] at off_w, bias colsum DS2 at off_b) of
   // its rows into slab s
