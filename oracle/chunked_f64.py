@@ -43,7 +43,7 @@ class ChunkedGraph:
     """The reference graph over N states held as float32 arrays on the host, evaluated chunk by chunk."""
 
     def __init__(self, spec: PolicySpec, X, actions, advant, old_dist, device="cpu", chunk=1 << 20,
-                 dtype=torch.float64):
+                 dtype=torch.float64, resident=False):
         self.spec = spec
         self.dt = dtype
         self.np_dt = np.float64 if dtype == torch.float64 else np.float32
@@ -51,6 +51,10 @@ class ChunkedGraph:
         self.N = int(X.shape[0])
         self.dev = torch.device(device)
         self.chunk = int(chunk)
+        self.resident = None
+        if resident:   # the batch copied to the device once, in the graph's dtype (timing runs)
+            f = lambda x, dt=self.dt: torch.as_tensor(np.ascontiguousarray(x), device=self.dev).to(dt)
+            self.resident = (f(X), f(actions, torch.int64), f(advant), f(old_dist))
 
     def _vars(self, theta, grad):
         out, off = [], 0
@@ -66,6 +70,9 @@ class ChunkedGraph:
     def _chunks(self):
         for lo in range(0, self.N, self.chunk):
             hi = min(self.N, lo + self.chunk)
+            if self.resident is not None:
+                yield tuple(t[lo:hi] for t in self.resident)
+                continue
             f = lambda x, dt=self.dt: torch.as_tensor(np.ascontiguousarray(x[lo:hi]), device=self.dev).to(dt)
             yield f(self.X), f(self.a, torch.int64), f(self.adv), f(self.old)
 
