@@ -4,7 +4,7 @@ TEST INFRASTRUCTURE ONLY.
 
 A child process because torch's bundled HIP runtime must start before the engine's in a process
 (trpo_amd/engine.py, rollout_fetch), and the test session has started the engine's long before.
-usage: python tests/bign_truth.py <old.npy> <out.npz>
+usage: python tests/bign_truth.py <old.npy> <out.npz> [c4|c3]
 The batch is regenerated from bign_data's seeds; old.npy is the engine's pi_old [N, A] f32 (the engine call's
 exact input). Advantages are the reference discount + standardisation of the rewards on equal-length paths."""
 import os
@@ -16,14 +16,15 @@ import torch
 torch.cuda.init()
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.dirname(HERE), HERE]
-from bign_data import PATH_LEN, SPEC, make_batch, make_rewards  # noqa: E402
+from bign_data import CONFIGS, PATH_LEN, make_batch, make_rewards  # noqa: E402
 from oracle.chunked_f64 import ChunkedGraph, advantages_equal_paths  # noqa: E402
 
 
-def main(old_path, out):
-    b = make_batch()
+def main(old_path, out, config="c4"):
+    SPEC, n = CONFIGS[config]
+    b = make_batch(n, SPEC)
     old = np.load(old_path, allow_pickle=False)
-    rewards, _ = make_rewards()
+    rewards, _ = make_rewards(n)
     adv = advantages_equal_paths(rewards, PATH_LEN)
     res = {}
     for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
@@ -36,4 +37,4 @@ def main(old_path, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *sys.argv[3:4])
