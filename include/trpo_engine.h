@@ -213,8 +213,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * f32 FMA; <= 32 actions, last hidden width 129..256; default 1), "head_fwd" (softmax head forwards with one state per lane on f32 FMAs,
  * hbwd.hip: 1 = the prepare and the line-search heads; 2 = the line-search heads, and the prepare head
  * when the head has <= 8 actions, the default; 0 = off), "splits" (split-K slabs of the FVP's weight
- * gradients; 0 = auto, 512 at C4) and "pg_splits" (the policy gradient's; 0 = auto, 4 x splits up to 2048): both are read when an engine is
- * created.
+ * gradients; 0 = auto: by tile count, at least one per 16k rows; 512 at C4, 245 at C5) and "pg_splits" (the
+ * policy gradient's; 0 = auto: 4 x splits or one per 4k rows, up to 2048): both are read when an engine
+ * is created.
  * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed
  * from the build in round 4; tools/patches/pruned_variants.patch restores them.
  * Process-wide. */

@@ -1,5 +1,5 @@
 """The synthetic full-size batches of the float64 whole-update tests (test_gpu_bigN.py: C4, 8M states;
-test_gpu_c3_full.py: C3, 1M states), shared with their float64 child process (tests/bign_truth.py), which
+test_gpu_full_size.py: C2 / C3 / C5), shared with their float64 child process (tests/bign_truth.py), which
 regenerates them from the same seeds instead of receiving gigabytes of inputs."""
 import numpy as np
 
@@ -8,7 +8,8 @@ from oracle import trpo_oracle as O
 N = 8_000_000
 SPEC = O.PolicySpec(128, [256, 256], 18)
 PATH_LEN = 200   # CartPole-v0 path length cap: an episode start every 200 states
-CONFIGS = {"c4": (SPEC, N), "c3": (O.PolicySpec(128, [64, 64], 18), 1_000_000)}
+CONFIGS = {"c4": (SPEC, N), "c3": (O.PolicySpec(128, [64, 64], 18), 1_000_000),
+           "c2": (O.PolicySpec(11, [64, 64], 3), 50_000), "c5": (O.PolicySpec(376, [1024, 1024], 17), 4_000_000)}
 
 
 def make_batch(n=N, spec=SPEC):

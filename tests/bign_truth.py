@@ -4,7 +4,7 @@ TEST INFRASTRUCTURE ONLY.
 
 A child process because torch's bundled HIP runtime must start before the engine's in a process
 (trpo_amd/engine.py, rollout_fetch), and the test session has started the engine's long before.
-usage: python tests/bign_truth.py <old.npy> <out.npz> [c4|c3]
+usage: python tests/bign_truth.py <old.npy> <out.npz> [c4|c3|c2|c5]
 The batch is regenerated from bign_data's seeds; old.npy is the engine's pi_old [N, A] f32 (the engine call's
 exact input). Advantages are the reference discount + standardisation of the rewards on equal-length paths."""
 import os

@@ -9,8 +9,11 @@ sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
 from oracle import trpo_oracle as O  # noqa: E402
 
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 8_000_000
-SPEC = O.PolicySpec(128, [256, 256], 18)
+from bign_data import CONFIGS  # noqa: E402
+
+CFG = sys.argv[1] if len(sys.argv) > 1 else "c4"
+SPEC, N = CONFIGS[CFG]
+SETS = sys.argv[2] if len(sys.argv) > 2 else "default"
 
 
 def rel(a, b):
@@ -87,6 +90,13 @@ def main():
         "bf16x6": {"split_f16": 0},
         "low_seg=0": {"low_seg": 0},
     }
+    if SETS == "c5":
+        sets = {
+            "default": {},
+            "pg_splits=1024": {"pg_splits": 1024},
+            "splits=256,pg=1024": {"splits": 256, "pg_splits": 1024},
+            "splits=512,pg=2048": {"splits": 512, "pg_splits": 2048},
+        }
     res = {}
     for name, opts in sets.items():
         res[name] = run(opts)

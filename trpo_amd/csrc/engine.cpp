@@ -374,11 +374,17 @@ struct trpo_engine {
     // the activations at HBM rate; small policies take up to 2048 splits while the slabs fit 128 MB
     if (tiles_max == 1)
       s_target = (int)std::max<int64_t>(s_target, std::min<int64_t>(2048, (int64_t(128) << 20) / (slab_stride * 4)));
+    // a split accumulates its rows in f32 MFMA accumulators, whose error grows with the rows per split (DESIGN.md
+    // §6, numerics at full size): at least one FVP split per 16k rows (wide layers: C5 64 -> 245), and for the
+    // policy gradient (once per update; its layer-0/1 blocks are sums of adv_n s_n with mean-zero advantages) 4x
+    // that and one per 4k rows, up to 2048; slabs within 2 GB / 8 GB
+    const int64_t slab_bytes = (int64_t)slab_stride * 4;
+    auto fit = [&](int64_t bytes) { return std::max<int64_t>(1, bytes / slab_bytes); };
+    s_target = (int)std::max<int64_t>(s_target, std::min<int64_t>(fit(int64_t(2) << 30), (cap + 16383) / 16384));
     if (g_options.splits > 0) s_target = std::min(g_options.splits, 8192);
-    // the policy gradient (once per update) takes 4x the splits, up to 2048: its layer-0/1 blocks are sums of
-    // adv_n s_n over the batch with mean-zero advantages, whose f32 MFMA accumulation error grows with the rows
-    // per split (numerics at 8M); the FVPs keep the faster geometry
-    int s_pg = std::max(s_target, std::min(2048, 4 * s_target));
+    int s_pg = (int)std::max<int64_t>(
+        s_target, std::min<int64_t>({2048, std::max<int64_t>(4 * (int64_t)s_target, (cap + 4095) / 4096),
+                                     fit(int64_t(8) << 30)}));
     if (g_options.pg_splits > 0) s_pg = std::min(g_options.pg_splits, 8192);
     slab = dalloc<float>((size_t)std::max(s_target, s_pg) * slab_stride);
     S = s_target;
