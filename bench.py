@@ -222,8 +222,10 @@ def tag_roof(tag: str, widths, n: int):
 
 
 def committed_traffic(config: str, rows: int, tag: str):
-    """Per-launch HBM bytes of `tag` from the newest matching profiles/*/traffic.json."""
-    best = None
+    """Per-launch HBM bytes of `tag` from profiles/*/traffic.json: the file measured on this source build if one
+    is committed, else the last matching one in name order."""
+    best = same = None
+    build = source_build_id()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
         try:
             d = json.load(open(f))
@@ -231,7 +233,9 @@ def committed_traffic(config: str, rows: int, tag: str):
             continue
         if d.get("config") == config and d.get("rows") == rows and tag in d.get("tags", {}):
             best = (os.path.relpath(f, ROOT), d["tags"][tag], d.get("build"))
-    return best
+            if d.get("build") == build:
+                same = best
+    return same or best
 
 
 def source_build_id() -> str:
