@@ -69,3 +69,21 @@ def test_world_size_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_committed_traffic_prefers_the_current_build(tmp_path, monkeypatch):
+    """The bench's roofline `traffic` comes from the committed PMC file measured on its own source build when
+    there is one (a later-named file of another build must not shadow it), else from the last file in name order."""
+    build = bench.source_build_id()
+    for name, b, val in (("r9a", build, 1.0), ("r9z", "0000000000000000", 2.0)):
+        d = tmp_path / "profiles" / name
+        d.mkdir(parents=True)
+        (d / "traffic.json").write_text(json.dumps({"config": "c4", "rows": 8, "build": b,
+                                                    "tags": {"fvp_x": {"bytes": val}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "source_build_id", lambda: build)
+    path, entry, b = bench.committed_traffic("c4", 8, "fvp_x")
+    assert path.endswith(os.path.join("r9a", "traffic.json")) and b == build and entry["bytes"] == 1.0
+    monkeypatch.setattr(bench, "source_build_id", lambda: "ffffffffffffffff")
+    path, entry, b = bench.committed_traffic("c4", 8, "fvp_x")
+    assert path.endswith(os.path.join("r9z", "traffic.json")) and entry["bytes"] == 2.0
