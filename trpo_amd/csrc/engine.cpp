@@ -617,6 +617,13 @@ struct trpo_engine {
     S_cur = s;
     set_splits();
   }
+  // the policy gradient's split geometry for one scope; the FVP's comes back on every exit, a throwing launch
+  // included
+  struct PgSplits {
+    trpo_engine* e;
+    explicit PgSplits(trpo_engine* en) : e(en) { e->use_splits(e->S_pg); }
+    ~PgSplits() { e->use_splits(e->S); }
+  };
   void set_splits() {
     // rows per split: a multiple of the 16-row k-tile, >= 64 rows
     const int smax = S_cur;
@@ -944,7 +951,7 @@ struct trpo_engine {
         hb.E1 = prep_e_top ? E[L - 2] : nullptr;
         hb.am_d1 = am_d(L - 2);
         hb.am_ds1 = am_ds(L - 2);
-        use_splits(S_pg);   // the slab block it writes is reduced with the policy gradient's
+        PgSplits pgs(this);   // the slab block it writes is reduced with the policy gradient's
         hb.splits = active_splits;
         hb.rows_per_split = rows_per_split;
         hb.slab = slab;   // the policy gradient's W_{L-1} / b_{L-1} block, reduced by policy_grad()
@@ -960,7 +967,6 @@ struct trpo_engine {
         Scope sp(this, "bwd2_l2");
         launch_head_bwd2(hb, num_cus, stream);
         check_launch();
-        use_splits(S);
         ds_ready = true;
         if (hb.D1h) {
           d1_plane = true;
@@ -1037,7 +1043,7 @@ struct trpo_engine {
   void policy_grad() {
     prepare();
     ensure_w3();
-    use_splits(S_pg);
+    PgSplits pgs(this);
     // surr backward: DS_{l-1} = (DS_l W_l^T)(1-H_l^2) ; DS of hidden layers lives in RD scratch
     std::vector<float*> DS(L);
     DS[L - 1] = DSL;
@@ -1082,7 +1088,6 @@ struct trpo_engine {
                   nullptr, t);
     }
     reduce_grad(g, nullptr);
-    use_splits(S);
   }
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
