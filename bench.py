@@ -261,6 +261,15 @@ def fvp_flops_per_row(widths) -> float:
     return f
 
 
+def update_flops_8d(widths, n: int) -> float:
+    """SURVEY.md §8(d)'s full update (k = 1): N*(grad + 11*FVP + 1*fwd), with grad = 4a1b1 + 6 sum_{l>=2} a_l b_l
+    and fwd = 2 sum_l a_l b_l."""
+    ab = [widths[l] * widths[l + 1] for l in range(len(widths) - 1)]
+    grad = 4 * ab[0] + 6 * sum(ab[1:])
+    fwd = 2 * sum(ab)
+    return float(n) * (grad + 11 * fvp_flops_per_row(widths) + fwd)
+
+
 def synthetic_theta(widths, rng) -> np.ndarray:
     """W ~ U(+-sqrt(6/(fan_in+fan_out))), b ~ N(0, 0.1^2), flat [W1,b1,...]."""
     parts = []
@@ -434,6 +443,52 @@ def comm_block(eng, world, rank, rehearsal, dist):
             "world": world, "distinct_devices": len(set(buses)), "per_rank": ranks}
 
 
+DIGEST_STATS = ("cg_iters", "k", "reverted", "shs", "lm", "rate", "rdotr", "gdotstepdir", "surr_after", "kl_after",
+                "ent_after")
+
+
+def rank_digest(vectors, stats) -> str:
+    """sha256 (16 hex) over the bytes of an update's replicated outputs: theta, g, stepdir and fullstep as
+    float32 arrays and the CG / step / line-search scalars (every rank must end an update
+    with bitwise-identical theta and CG scalars, since the CG and line-search branches run redundantly)."""
+    import hashlib
+    import struct
+    h = hashlib.sha256()
+    for v in vectors:
+        h.update(np.ascontiguousarray(v, dtype=np.float32).tobytes())
+    for k in DIGEST_STATS:
+        h.update(k.encode())
+        h.update(struct.pack("<d", float(stats[k])))
+    return h.hexdigest()[:16]
+
+
+def engine_digest(eng, stats) -> str:
+    from trpo_amd._lib import VEC_FULLSTEP, VEC_G, VEC_STEPDIR, VEC_THETA
+    return rank_digest([eng.get_vector(w) for w in (VEC_THETA, VEC_G, VEC_STEPDIR, VEC_FULLSTEP)], stats)
+
+
+def gather_rank_check(digest: str, fvp_ms: float, world: int, dist) -> dict:
+    """All-gather every rank's update digest and FVP time (outside the timed region).  The result goes into
+    the line's `comm` block; `ranks_bitwise_equal` is False when any rank's digest differs."""
+    mine = {"digest": digest, "fvp_ms": fvp_ms}
+    allr = [mine]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    digests = [r["digest"] for r in allr]
+    return {"ranks_bitwise_equal": len(set(digests)) == 1, "rank_digests": digests,
+            "fvp_ms_per_rank": [r["fvp_ms"] for r in allr]}
+
+
+def enforce_rank_check(check: dict):
+    """Exit non-zero (status 3) when the ranks' updates differ: a multi-GPU line whose ranks diverged is
+    not a measurement of the algorithm."""
+    if not check["ranks_bitwise_equal"]:
+        sys.stderr.write(f"bench.py: ranks ended the update with different bits: {check['rank_digests']}\n")
+        sys.stderr.flush()
+        raise SystemExit(3)
+
+
 def launch_ranks(argv, gpus: int, rehearsal: bool, visible_gpus: int) -> int:
     """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N ranks on this node as one child
     process (`python -m torch.distributed.run`, rendezvous on 127.0.0.1), relay their output and return
@@ -537,11 +592,17 @@ def main():
     eng = wl.engine(comm_setup)
     comm = comm_block(eng, world, rank, rehearsal, dist)
     elapsed, last = timed_updates(eng, wl, args.steps, args.warmup, barrier)
+    digest = engine_digest(eng, last)   # after the timed region: the last timed update's outputs
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     prof = profile_pass(eng, wl, max(1, args.profile_steps))
+    fvp_tags, fvp_calls = fvp_tags_per_call(prof)
+    fvp_ms = sum(ms for _, (_, ms) in fvp_tags.items()) + prof.get("reduce", [0, 0])[1] * (
+        fvp_calls / max(1, prof.get("reduce", [1, 1])[0]))
+    fvp_s = fvp_ms / max(1, fvp_calls) / 1e3 if fvp_calls else float("nan")
+    comm.update(gather_rank_check(digest, fvp_s * 1e3, world, dist))
     num_params = eng.num_params
     prod = split_products()
     eng.close()
@@ -587,14 +648,11 @@ def main():
         dom_prod = 6 if dom in ("fvp_chain", "fvp_fused") else prod   # chain / fused: exact bf16 x6 split
         peak_basis = (f"split MFMA: f16/bf16 dense peak 2.5 PF / {dom_prod} products" if tag_is_split(dom, widths)
                       else "f32 MFMA peak")
-        upd_flops = sum(tag_flops(t, widths, n) * c for t, (c, _) in kernel_tags.items()) / psteps
-        upd_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / psteps
+        upd_own_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / psteps
         tr = committed_traffic(args.config, N, dom) if world == 1 else None
         upd_s = elapsed / args.steps
-        fvp_tags, fvp_calls = fvp_tags_per_call(prof)
-        fvp_ms = sum(ms for _, (_, ms) in fvp_tags.items()) + prof.get("reduce", [0, 0])[1] * (
-            fvp_calls / max(1, prof.get("reduce", [1, 1])[0]))
-        fvp_s = fvp_ms / max(1, fvp_calls) / 1e3 if fvp_calls else float("nan")
+        upd_flops_8d = update_flops_8d(widths, N)          # the whole job's (all ranks') §8(d) FLOPs
+        upd_peak = peak   # the dominant (FVP) kernel's issued arithmetic: f16x3 833.3, bf16x6 416.7 or f32 157.3
         fvp_alg_bytes = n * cfg["obs"] * 4 + 3 * num_params * 4
         fvp_moved = sum(tag_bytes(t, widths, n) * c for t, (c, _) in fvp_tags.items()) / max(1, fvp_calls)
         # the split actually issued: the wide GEMMs' (f16x3 or bf16x6) unless the whole FVP is one fused
@@ -648,7 +706,7 @@ def main():
                          "flops_per_launch": fl, "avg_launch_ms": avg_s * 1e3, "launches": cnt,
                          "algorithmic_bytes_per_launch": alg_by,
                          "algorithmic_bytes_frac": alg_by / avg_s / 1e9 / PEAK_HBM_GBS,
-                         "own_bound": bound,
+                         "own_bytes_bound": bound,
                          "own_traffic_bytes_per_launch": by,
                          "own_traffic_hbm_gbs": by / avg_s / 1e9,
                          "own_traffic_hbm_frac": by / avg_s / 1e9 / PEAK_HBM_GBS,
@@ -657,10 +715,18 @@ def main():
                          "traffic_build": tr[2] if tr else None,
                          "build": source_build_id(),
                          "traffic_same_build": bool(tr and tr[2] == source_build_id())},
-            "update_roofline": {"algorithmic_tflop_per_update": upd_flops * world / 1e12,
-                                "achieved_tflops": upd_flops * world / upd_s / 1e12,
-                                "roof_ms_per_update": upd_peak_s * 1e3,
-                                "frac_of_roof": upd_peak_s / upd_s},
+            "update_roofline": {"algorithmic_tflop_per_update": upd_flops_8d / 1e12,
+                                "achieved_tflops": upd_flops_8d / upd_s / 1e12,
+                                "peak_tflops": upd_peak,
+                                "roof_ms_per_update": upd_flops_8d / (upd_peak * 1e12) * 1e3,
+                                "frac": upd_flops_8d / upd_s / 1e12 / upd_peak,
+                                "frac_of_f32_peak": upd_flops_8d / upd_s / 1e12 / PEAK_F32_TFLOPS,
+                                "basis": "SURVEY.md §8(d): N*(grad + 11*FVP + 1*fwd) FLOPs per update (grad = "
+                                         "4a1b1 + 6 sum a_l b_l, FVP = 4a1b1 + 12 sum, fwd = 2 sum over layers) / "
+                                         "ms_per_step / the dense peak of the arithmetic the dominant FVP kernel issues "
+                                         "(frac_of_f32_peak: against §8(d)'s fp32 roof)",
+                                "own_bytes_roof_ms_per_update": upd_own_peak_s * 1e3,
+                                "own_bytes_frac_of_roof": upd_own_peak_s / upd_s},
             "fvp": {"ms_per_fvp": fvp_s * 1e3,
                     "gbps_algorithmic": fvp_alg_bytes / fvp_s / 1e9,
                     "hbm_frac_algorithmic": fvp_alg_bytes / fvp_s / 1e9 / PEAK_HBM_GBS,
@@ -688,6 +754,7 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    enforce_rank_check(comm)
 
 
 if __name__ == "__main__":

@@ -87,3 +87,58 @@ def test_committed_traffic_prefers_the_current_build(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "source_build_id", lambda: "ffffffffffffffff")
     path, entry, b = bench.committed_traffic("c4", 8, "fvp_x")
     assert path.endswith(os.path.join("r9z", "traffic.json")) and entry["bytes"] == 2.0
+
+
+def _rank_check_worker(rank, world, port, digests, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        chk = bench.gather_rank_check(digests[rank], 10.0 + rank, world, dist)
+        try:
+            bench.enforce_rank_check(chk)
+            code = 0
+        except SystemExit as e:
+            code = e.code
+        q.put((rank, chk, code))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("digests,equal", [(("aa", "aa"), True), (("aa", "ab"), False)])
+def test_rank_check_two_gloo_ranks(digests, equal):
+    """World-size-2 gloo: bench.py's post-timing self-check gathers every rank's update digest and FVP time;
+    differing digests give ranks_bitwise_equal = False and exit status 3 on every rank."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_check_worker, args=(r, 2, port, digests, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, chk, code in outs:
+        assert chk["ranks_bitwise_equal"] is equal
+        assert chk["rank_digests"] == list(digests)
+        assert chk["fvp_ms_per_rank"] == [10.0, 11.0]
+        assert code == (0 if equal else 3)
+
+
+def test_rank_digest_sees_every_bit():
+    import numpy as np
+    stats = {k: 1.0 for k in bench.DIGEST_STATS}
+    v = [np.arange(10, dtype=np.float32), np.ones(10, np.float32)]
+    d0 = bench.rank_digest(v, stats)
+    assert d0 == bench.rank_digest([x.copy() for x in v], dict(stats))
+    w = v[0].copy()
+    w.view(np.uint32)[3] ^= 1                      # one ulp of one element
+    assert bench.rank_digest([w, v[1]], stats) != d0
+    assert bench.rank_digest(v, dict(stats, rdotr=np.nextafter(1.0, 2.0))) != d0

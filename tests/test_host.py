@@ -47,3 +47,33 @@ def test_paths_to_batch_concatenates_and_marks_starts():
     assert b["state"].shape == (5, 4) and b["action_dist"].shape == (5, 2)
     np.testing.assert_array_equal(b["starts"], [1, 0, 0, 1, 0])
     np.testing.assert_array_equal(b["baseline"], [0, 0, 0, .5, .25])
+
+
+class _CommRecorder:
+    def __init__(self):
+        self.calls = []
+
+    def comm_set_host_allreduce(self, fn, rank, world):
+        self.calls.append((rank, world))
+
+
+def test_set_ranks_after_vf_exists_hooks_the_existing_net():
+    """set_ranks called once the VF net exists (after a fit) must sum that net's gradient too,
+    not only a net created later."""
+    from types import SimpleNamespace
+    from trpo_amd.agent import TRPOAgent
+    net = _CommRecorder()
+    fake = SimpleNamespace(engine=_CommRecorder(), vf=SimpleNamespace(net=net, on_create=None))
+    TRPOAgent.set_ranks(fake, 1, 2, group=None, host_allreduce=True)
+    assert fake.engine.calls == [(1, 2)]
+    assert net.calls == [(1, 2)]                 # the existing net, hooked at once
+    later = _CommRecorder()
+    fake.vf.on_create(later)                     # and any net created afterwards
+    assert later.calls == [(1, 2)]
+
+
+def test_rollout_seeds_never_collide_across_ranks():
+    from trpo_amd.agent import rollout_seed
+    seen = {rollout_seed(1, i, r) for r in range(8) for i in range(100_000)}
+    assert len(seen) == 8 * 100_000
+    assert rollout_seed(1, 5, 0) == 1 * 1000003 + 5        # rank 0 keeps the one-rank stream

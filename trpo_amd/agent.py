@@ -89,6 +89,12 @@ def paths_to_batch(paths: List[Dict]) -> Dict[str, np.ndarray]:
     return out
 
 
+def rollout_seed(seed: int, iteration: int, rank: int) -> int:
+    """The Philox key of one rank's rollout at one iteration: ranks live 2^40 keys apart, so no rank
+    ever draws another rank's stream at any reachable iteration count."""
+    return (seed * 1000003 + iteration + (rank << 40)) & ((1 << 64) - 1)
+
+
 class TRPOAgent:
     def __init__(self, obs_dim: int, n_actions: int, hidden: Sequence[int] = (64,), max_rows: int = 4096,
                  device: int = 0, theta: Optional[np.ndarray] = None, config: Optional[dict] = None,
@@ -136,6 +142,8 @@ class TRPOAgent:
                 net.comm_init(broadcast_unique_id(Engine.comm_unique_id, self.rank, group), self.rank, self.world)
 
         self.vf.on_create = vf_comm
+        if self.vf.net is not None:   # set_ranks after a fit: the existing net's gradient is summed from now on
+            vf_comm(self.vf.net)
 
     def _host_sum(self, *vals: float) -> np.ndarray:
         """Sum of host scalars over the ranks (gloo), float64; identity for one rank."""
@@ -224,7 +232,7 @@ class TRPOAgent:
                 inj = {"reset_uniforms": ru, "action_uniforms": au, "max_episodes_per_env": me}
             n, n_paths = eng.rollout_cartpole(n_envs=n_envs, n_timesteps=n_timesteps,
                                               max_pathlength=cfg["max_steps"],
-                                              seed=seed * 1000003 + i + 7919 * self.rank,
+                                              seed=rollout_seed(seed, i, self.rank),
                                               train=self.train, **inj)                   # :96-100
             n_global = int(self._host_sum(n)[0])
             eng.rollout_to_batch(n_global=n_global)                                      # :108-122

@@ -1015,7 +1015,11 @@ struct trpo_engine {
     allreduce_f32(out, (size_t)P);
   }
 
-  void wgrad_layer(int l, int nseg, WSeg s0, WSeg s1, int colsum_seg, const int* skip, const char* tag) {
+  // every slab writer other than the policy gradient's own layers clears ds_ready: the head-layer block and
+  // DS_{L-2} that prepare() leaves for policy_grad() (hbwd.hip) are then recomputed instead of trusted
+  void wgrad_layer(int l, int nseg, WSeg s0, WSeg s1, int colsum_seg, const int* skip, const char* tag,
+                   bool keeps_pg_head = false) {
+    if (!keeps_pg_head) ds_ready = false;
     WGradArgs a{};
     a.rows = (int)n;
     a.Ma = w[l];
@@ -1085,7 +1089,7 @@ struct trpo_engine {
       char t[32];
       std::snprintf(t, sizeof t, "pg_wgrad_l%d", l);
       wgrad_layer(l, 1, WSeg{act_in(l), DS[l], wp[l], wp[l + 1], l == 0 ? am_x() : nullptr, am_ds(l)}, WSeg{}, 0,
-                  nullptr, t);
+                  nullptr, t, /*keeps_pg_head=*/true);
     }
     reduce_grad(g, nullptr);
   }
@@ -1203,6 +1207,7 @@ struct trpo_engine {
       char tag[32];
       std::snprintf(tag, sizeof tag, "fvp_tail_l%d", l);
       Scope sp(this, tag);
+      ds_ready = false;   // slab and RD writer
       launch_tail_pack(tp, stream);
       launch_fvp_tail(ta, stream);
       check_launch();
@@ -1228,6 +1233,7 @@ struct trpo_engine {
           a.am_a1 = am_d(1);
           a.E = E[0];
           a.RH = RH[1];
+          ds_ready = false;   // slab writer
           Scope sp(this, "fvp_rbwdwg_l1");
           launch_rbwd0(a, stream);
           check_launch();

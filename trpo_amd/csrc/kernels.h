@@ -10,8 +10,10 @@
 
 namespace trpo {
 
-// Kernel-variant switches (defaults from TRPO_ROWCFG / TRPO_WGCFG / TRPO_FUSED_HEAD /
-// TRPO_HEAD_BWD; runtime-settable through trpo_set_option for A/B and parity tests).
+// Kernel-variant switches (defaults from TRPO_SPLIT_MFMA, TRPO_SPLIT_WG, TRPO_CHAIN, TRPO_SPLIT_F16,
+// TRPO_SPLIT_MIN_K, TRPO_GRAPHS, TRPO_TAIL, TRPO_FUSED, TRPO_LOW_SEG, TRPO_PLANES, TRPO_RBWD0, TRPO_HBWD2,
+// TRPO_HEAD_FWD, TRPO_SPLITS, TRPO_PG_SPLITS in gemm.hip; runtime-settable through trpo_set_option for A/B
+// and parity tests).
 struct Options {
   int split_mfma;  // row GEMMs with N > 128 on the split MFMA: 0 off (f32 MFMA), 5 = 256 x 256 tile at
                    // BK 32 on f16 planes (default), 6 = 256 x 256 at BK 16, any other value = 128 x 256
@@ -30,11 +32,11 @@ struct Options {
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
   int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
                    // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
-  int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (1 prepare + line search, 2 line
-                   // search, and the prepare head when the head has <= 8 actions)
+  int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (hbwd.hip) instead of the
+                   // f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 prepare + line search, 2 line
+                   // search, and the prepare head when the head has <= 8 actions
   int splits;      // engine: weight-gradient split-K slabs of the FVP launches (0 = auto: 512 at C4)
   int pg_splits;   // engine: the policy gradient's split-K slabs (0 = auto: 4 x splits, at most 2048)
-                   // (hbwd.hip) instead of the f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
