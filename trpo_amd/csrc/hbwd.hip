@@ -173,6 +173,182 @@ __global__ void __launch_bounds__(kHbThreads) head_bwd2_kernel(const HeadBwd2Arg
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// The same three contractions on f32 MFMA (option hbwd2 = 2): v_mfma_f32_32x32x2_f32 is exact f32, the fmaf
+// chains' own arithmetic (MI355X_MICROARCH.md), but one instruction does 2 x 32 x 32 of them with operands
+// in registers, where the kernel above spends one LDS broadcast and three VALU FMAs per action, row and
+// column (2.55e9 VALU instructions per C4 launch, VALU-issue bound: profiles/r4ao).
+//   * 8 waves; wave w owns hidden columns [32w, 32w + 32); 32-row tiles of the workgroup's split.
+//   * D / DS: C[row][col] = sum_j D2[row][j] W[col][j]: A = the tile's D2 / DS2 rows from LDS (lane = row,
+//     k = j), B = W^T held in registers for the launch (lane = column, k = j): k-step s takes actions 2s, 2s+1,
+//     so each output is the fmaf chain j = 0, 1, .. of the VALU kernel.
+//   * the outputs come out in C layout (lane = column, registers = rows), the layout H is loaded in for
+//     (1 - H^2) and the row-coalesced stores.
+//   * weight gradient H^T DS2 (K = rows): A = H's C-layout registers themselves (k-step s = register s: lane
+//     half h supplies row (s&3) + 8(s>>2) + 4h), B = DS2 from LDS at the same rows (lane = action).
+// ---------------------------------------------------------------------------------------------------------
+constexpr int kHmW = 8;   // waves
+
+__device__ __forceinline__ float ldbf(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+
+template <int K2>   // k-steps of the action contraction: ceil(A / 2)
+__global__ void __launch_bounds__(kHmW * 64, 2) head_bwd2m_kernel(const HeadBwd2Args a) {
+  __shared__ float sd[2][kHbRows][kHbA + 1];   // the tile's D2 / DS2 rows, zero past A (pad: conflict-free reads)
+  __shared__ float sred[3][kHmW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  const int col = 32 * w + lr;
+  const bool cv = col < a.Npad;
+  constexpr int kOob = 0x40000000;
+  const int vo = cv ? ((4 * lh) * a.Npad + col) * 4 : kOob;   // C layout: lane = column, register i = row r(i)
+  auto roff = [](int i) { return (i & 3) + 8 * (i >> 2); };
+  // W^T in registers: k-step s, lane half h -> action 2s + h
+  float wf[K2];
+#pragma unroll
+  for (int s = 0; s < K2; ++s) {
+    const int j = 2 * s + lh;
+    wf[s] = (cv && j < a.A) ? a.WB[(size_t)j * a.Npad + col] : 0.0f;
+  }
+  const bool wg = a.slab != nullptr;
+  f32x16 gw = f32x16{};   // H^T DS2 over the split: lane = action, registers = columns 32w + r(i) + 4h
+  float gb = 0.0f;        // DS2 column sums (thread j < A)
+  float mx1 = 0.0f, mx2 = 0.0f;
+  const int r0 = blockIdx.x * a.rows_per_split;
+  const int r1 = min(a.rows, r0 + a.rows_per_split);
+  auto desc = [&](const void* p, int t0, int ld, int esz) {
+    const int nr = max(0, min(kHbRows, r1 - t0));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p + (size_t)t0 * ld * esz), 0, nr * ld * esz,
+                                             0x00020000);
+  };
+  // one tile ahead in registers: the H column block and this thread's share of the head deltas
+  constexpr int kSt = 2 * kHbRows * kHbA / (kHmW * 64);   // 4
+  float hc[16], pc[kSt];
+  auto load = [&](int t0, float (&hv)[16], float (&pv)[kSt]) {
+    const __amdgpu_buffer_rsrc_t rH = desc(a.H, t0, a.Npad, 4);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) hv[i] = ldbf(rH, vo, roff(i) * a.Npad * 4);
+    const __amdgpu_buffer_rsrc_t rD = desc(a.D2, t0, a.Apad, 4), rS = desc(a.DS2, t0, a.Apad, 4);
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) {
+      const int i = tid + u * kHmW * 64;
+      const int m = i / (kHbRows * kHbA), r = (i / kHbA) % kHbRows, j = i % kHbA;
+      const int v = j < a.A ? (r * a.Apad + j) * 4 : kOob;
+      pv[u] = ldbf(m ? rS : rD, v, 0);
+    }
+  };
+  if (r0 < r1) load(r0, hc, pc);
+  for (int t0 = r0; t0 < r1; t0 += kHbRows) {
+    const int tile = t0 / kHbRows;
+    __syncthreads();   // the previous tile's deltas are consumed
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) {
+      const int i = tid + u * kHmW * 64;
+      const int m = i / (kHbRows * kHbA), r = (i / kHbA) % kHbRows, j = i % kHbA;
+      sd[m][r][j] = pc[u];
+    }
+    float h[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h[i] = hc[i];
+    __syncthreads();
+    if (t0 + kHbRows < r1) load(t0 + kHbRows, hc, pc);   // in flight during this tile's MFMAs
+    // D / DS: the fmaf chains over the actions, two per MFMA
+    f32x16 ad = f32x16{}, as = f32x16{};
+#pragma unroll
+    for (int s = 0; s < K2; ++s) {
+      ad = __builtin_amdgcn_mfma_f32_32x32x2f32(sd[0][lr][2 * s + lh], wf[s], ad, 0, 0, 0);
+      as = __builtin_amdgcn_mfma_f32_32x32x2f32(sd[1][lr][2 * s + lh], wf[s], as, 0, 0, 0);
+    }
+    // the policy gradient's last-layer weight gradient: this tile's partial (one f32 chain per tile, added to
+    // the split's sums once: a split is thousands of rows)
+    if (wg) {
+      f32x16 g = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        g = __builtin_amdgcn_mfma_f32_32x32x2f32(h[s], sd[1][roff(s) + 4 * lh][lr], g, 0, 0, 0);
+      gw += g;
+      if (tid < a.A) {
+        float tb = 0.0f;
+#pragma unroll 8
+        for (int r = 0; r < kHbRows; ++r) tb += sd[1][r][tid];   // rows past the end were staged as 0
+        gb += tb;
+      }
+    }
+    const __amdgpu_buffer_rsrc_t rD1 = desc(a.D1, t0, a.Npad, 4), rS1 = desc(a.DS1, t0, a.Npad, 4);
+    const __amdgpu_buffer_rsrc_t rE1 = desc(a.E1 ? a.E1 : a.D1, t0, a.Npad, 4);
+    float tm = 0.0f;
+    float o1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float hh = h[i];
+      const float om = (1.0f - hh) * (1.0f + hh);
+      o1[i] = ad[i] * om;
+      const float o2 = as[i] * om;
+      const int so = roff(i) * a.Npad * 4;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o1[i]), rD1, vo, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o2), rS1, vo, so, 0);
+      if (a.E1)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, -2.0f * ad[i] * hh), rE1, vo, so, 0);
+      mx1 = fmaxf(mx1, fabsf(o1[i]));   // rows past the end: H = 0 and D2 = 0 -> 0
+      mx2 = fmaxf(mx2, fabsf(o2));
+      tm = fmaxf(tm, fabsf(o1[i]));
+    }
+    if (a.D1h) {
+      // D_1's hi plane with the tile's scale: max |D| over its rows and every column
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) tm = fmaxf(tm, __shfl_xor(tm, off, 64));
+      if (lane == 0) sred[2][w] = tm;
+      __syncthreads();
+      float m = 0.0f;
+#pragma unroll
+      for (int u = 0; u < kHmW; ++u) m = fmaxf(m, sred[2][u]);
+      const int e = f16_scale_exp(m);
+      const float sc = __builtin_ldexpf(1.0f, e);
+      if (tid == 0) a.eD1t[tile] = e;
+      // k-blocked [column / 32][row][32]: this wave's block, rows t0 .. (past the end: dropped)
+      const int nr = max(0, min(kHbRows, r1 - t0));
+      const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.D1h + ((size_t)w * a.d1_mpad + t0) * 32), 0, cv ? nr * 64 : 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)(o1[i] * sc)), rP,
+                                              ((roff(i) + 4 * lh) * 32 + lr) * 2, 0, 0);
+    }
+  }
+  if (wg) {
+    float* out = a.slab + (size_t)blockIdx.x * a.slab_stride;
+    if (lr < a.A) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = 32 * w + roff(i) + 4 * lh;
+        if (c < a.N) out[a.off_w + (int64_t)c * a.A + lr] = gw[i];
+      }
+    }
+    if (tid < a.A) out[a.off_b + tid] = gb;
+  }
+  // running maxima of both outputs (the f16 split scales of their consumers): one atomicMax per workgroup
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx1 = fmaxf(mx1, __shfl_xor(mx1, off, 64));
+    mx2 = fmaxf(mx2, __shfl_xor(mx2, off, 64));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    sred[0][w] = mx1;
+    sred[1][w] = mx2;
+  }
+  __syncthreads();
+  if (tid < 2) {
+    unsigned* slot = tid == 0 ? a.am_d1 : a.am_ds1;
+    if (slot) {
+      float m = 0.0f;
+#pragma unroll
+      for (int u = 0; u < kHmW; ++u) m = fmaxf(m, sred[tid][u]);
+      if (m > 0.0f) atomicMax(slot + (blockIdx.x % kAmaxSub) * kAmaxStride, __float_as_uint(m));
+    }
+  }
+}
+
 }  // namespace
 
 bool head_bwd2_eligible(int A, int Npad) { return A <= kHbA && Npad <= kHbThreads && Npad % 4 == 0; }
@@ -187,6 +363,16 @@ void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s) {
   if (a.splits <= 0 || a.rows_per_split % kHbRows || (int64_t)a.splits * a.rows_per_split < a.rows)
     throw std::runtime_error("head_bwd2: splits do not cover the rows in 32-row tiles");
   const int grid = a.splits;
+  if (g_options.hbwd2 == 2) {
+    switch ((a.A + 1) / 2) {
+#define HBM_CASE(k) case k: hipLaunchKernelGGL(head_bwd2m_kernel<k>, dim3(grid), dim3(kHmW * 64), 0, s, a); break;
+      HBM_CASE(1) HBM_CASE(2) HBM_CASE(3) HBM_CASE(4) HBM_CASE(5) HBM_CASE(6) HBM_CASE(7) HBM_CASE(8)
+      HBM_CASE(9) HBM_CASE(10) HBM_CASE(11) HBM_CASE(12) HBM_CASE(13) HBM_CASE(14) HBM_CASE(15)
+      default: hipLaunchKernelGGL(head_bwd2m_kernel<16>, dim3(grid), dim3(kHmW * 64), 0, s, a); break;
+#undef HBM_CASE
+    }
+    return;
+  }
   switch ((a.A + 3) / 4) {
     case 1: hipLaunchKernelGGL(head_bwd2_kernel<4>, dim3(grid), dim3(kHbThreads), 0, s, a); break;
     case 2: hipLaunchKernelGGL(head_bwd2_kernel<8>, dim3(grid), dim3(kHbThreads), 0, s, a); break;

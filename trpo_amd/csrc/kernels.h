@@ -31,7 +31,8 @@ struct Options {
   int rbwd0;       // engine: layer 1's R-backward (and the policy gradient's backward into layer 0) fused
                    // with layer 0's weight gradient where eligible (rbwd0.hip): 0 off, 1 on
   int hbwd2;       // engine: the prepare pass's and the policy gradient's backward through the head layer in one
-                   // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on
+                   // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on VALU fmaf
+                   // chains, 2 (default) on f32 MFMA
   int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (hbwd.hip) instead of the
                    // f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 prepare + line search, 2 line
                    // search, and the prepare head when the head has <= 8 actions
