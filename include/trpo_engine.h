@@ -210,7 +210,8 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * "hbwd2" (1 = the prepare pass's and the policy gradient's backward through the softmax head's layer
  * run as one launch of hbwd.hip over one read of H_{L-1}, which also writes D_{L-2}'s f16 hi plane for
  * rbwd0 (or E_{L-2} where the FVP path reads it) and the policy gradient's head-layer weight gradient;
- * f32 FMA; <= 32 actions, last hidden width 129..256; default 1), "head_fwd" (softmax head forwards with one state per lane on f32 FMAs,
+ * <= 32 actions, last hidden width 129..256; 2 = on f32 MFMA, the default; 1 = on VALU f32 FMA chains),
+ * "head_fwd" (softmax head forwards with one state per lane on f32 FMAs,
  * hbwd.hip: 1 = the prepare and the line-search heads; 2 = the line-search heads, and the prepare head
  * when the head has <= 8 actions, the default; 0 = off), "splits" (split-K slabs of the FVP's weight
  * gradients; 0 = auto: by tile count, at least one per 16k rows; 512 at C4, 245 at C5) and "pg_splits" (the

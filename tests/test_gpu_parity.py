@@ -283,6 +283,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
     {"hbwd2": 0}, {"hbwd2": 0, "chain": 0},                   # separate head backwards (prepare / policy gradient)
+    {"hbwd2": 1},                                             # the dual head backward on VALU fmaf chains
     {"head_fwd": 0}, {"head_fwd": 1}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
     {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -813,7 +814,8 @@ def test_rbwd0_fused_vs_per_layer_and_oracle(gpu_available, obs, hidden, A, n):
 def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
     """hbwd.hip: the prepare pass's D_{L-2} and the policy gradient's DS_{L-2} in one read of H (and D_1's f16 hi
     plane scaled per 32-row tile, or E_{L-2} where the fused FVP reads it) against the two row-GEMM backwards
-    (option hbwd2 = 0) and the float64 oracle: g, Hv and a whole update (trpo_inksci.py:54,56-70,144-158)."""
+    (option hbwd2 = 0) and the float64 oracle, on f32 MFMA (hbwd2 = 2, the default) and on VALU fmaf chains
+    (hbwd2 = 1): g, Hv and a whole update (trpo_inksci.py:54,56-70,144-158)."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     no_tail = n < 0                       # negative n: the same rows with the fused tail off
@@ -831,7 +833,7 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
         set_option("tail", 0)
     out = {}
     try:
-        for mode in (1, 0):
+        for mode in (2, 1, 0):
             set_option("hbwd2", mode)
             e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
             e.set_flat(dd["theta"])
@@ -845,7 +847,7 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
     finally:
         set_option("hbwd2", saved)
         set_option("tail", saved_tail)
-    for mode in (1, 0):
+    for mode in (2, 1, 0):
         g, hv, g2, st, theta = out[mode]
         assert_vec_close(g, gref, REL, f"g hbwd2={mode}")
         assert_vec_close(g2, gref, REL, f"g after fvp hbwd2={mode}")
@@ -853,3 +855,4 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
         assert st["k"] == r.k
         assert_vec_close(theta, r.theta_new, REL, f"theta hbwd2={mode}")
     assert_vec_close(out[1][0], out[0][0], REL, "dual vs row-GEMM backward g")
+    assert_vec_close(out[2][0], out[0][0], REL, "f32 MFMA dual vs row-GEMM backward g")
