@@ -138,10 +138,26 @@ def tag_is_split(tag: str, widths) -> bool:
     return get_option("split_mfma") != 0 and out > 128 and not head
 
 
+def fused16_used(widths) -> bool:
+    """Whether the one-launch FVP runs on the f16 split (engine.cpp use_fused16, fused16.hip fused16_eligible)."""
+    from trpo_amd._lib import get_option
+    w = widths
+    return (get_option("fused") == 3 and get_option("split_f16") != 0 and len(w) == 4 and 1 <= w[0] <= 128 and
+            48 < w[1] <= 64 and 48 < w[2] <= 64 and 1 <= w[3] <= 32)
+
+
+def tag_products(tag: str, widths) -> int:
+    """MFMA products per fp32 product of a split kernel: chain.hip / fused.hip take the exact bf16 hi+mid+lo
+    split (6), fused16.hip the scaled f16 hi+lo (3), the row GEMMs the engine's split option."""
+    if tag == "fvp_chain" or (tag == "fvp_fused" and not fused16_used(widths)):
+        return 6
+    return 3 if tag == "fvp_fused" else split_products()
+
+
 def tag_peak(tag: str, widths) -> float:
-    if tag in ("fvp_chain", "fvp_fused"):   # chain.hip / fused.hip: the exact bf16 hi+mid+lo split (6 products)
-        return PEAK_BF16_TFLOPS / 6
-    return peak_split_tflops() if tag_is_split(tag, widths) else PEAK_F32_TFLOPS
+    if tag_is_split(tag, widths):
+        return PEAK_BF16_TFLOPS / tag_products(tag, widths)
+    return PEAK_F32_TFLOPS
 
 
 def tag_bytes(tag: str, widths, n: int) -> float:
@@ -645,7 +661,7 @@ def main():
         peak = tag_peak(dom, widths)
         achieved = fl / avg_s / 1e12
         bound, _ = tag_roof(dom, widths, n)   # max(own bytes / HBM peak, FLOPs / MFMA peak)
-        dom_prod = 6 if dom in ("fvp_chain", "fvp_fused") else prod   # chain / fused: exact bf16 x6 split
+        dom_prod = tag_products(dom, widths)
         peak_basis = (f"split MFMA: f16/bf16 dense peak 2.5 PF / {dom_prod} products" if tag_is_split(dom, widths)
                       else "f32 MFMA peak")
         upd_own_peak_s = sum(tag_roof(t, widths, n)[1] * c for t, (c, _) in kernel_tags.items()) / psteps
@@ -656,9 +672,10 @@ def main():
         fvp_alg_bytes = n * cfg["obs"] * 4 + 3 * num_params * 4
         fvp_moved = sum(tag_bytes(t, widths, n) * c for t, (c, _) in fvp_tags.items()) / max(1, fvp_calls)
         # the split actually issued: the wide GEMMs' (f16x3 or bf16x6) unless the whole FVP is one fused
-        # launch (bf16x6) and no other kernel is a split GEMM
+        # launch (fused.hip bf16x6, fused16.hip f16x3) and no other kernel is a split GEMM
         wide_split = any(tag_is_split(t, widths) for t in kernel_tags if t not in ("fvp_chain", "fvp_fused"))
-        arith = ("f16x3" if prod == 3 else "bf16x6") if wide_split else "bf16x6"
+        fvp_prod = tag_products("fvp_fused" if "fvp_fused" in kernel_tags else "fvp_chain", widths)
+        arith = ("f16x3" if prod == 3 else "bf16x6") if wide_split else ("f16x3" if fvp_prod == 3 else "bf16x6")
         value = args.steps / elapsed
         metric = METRIC
         out = {
@@ -679,7 +696,9 @@ def main():
                            "other's, the O(eps) KL_ff terms, on one product)" if prod == 3 else
                            "fp32 in HBM and f32 accumulation; GEMMs wider than 128 columns on bf16 MFMA with "
                            "each fp32 operand split exactly into hi+mid+lo bf16 pieces (6 products)") +
-                          ("; the one-launch FVP (fused.hip) on the exact bf16 hi+mid+lo split (6 products)"
+                          (("; the one-launch FVP (fused16.hip) on the scaled f16 hi+lo split (3 products)"
+                            if fvp_prod == 3 else
+                            "; the one-launch FVP (fused.hip) on the exact bf16 hi+mid+lo split (6 products)")
                            if "fvp_fused" in kernel_tags else "") +
                           "; narrower GEMMs on f32 MFMA; softmax heads and CG scalars in f64",
             "data": "synthetic (X~N(0,1), a~U{0..A-1}, rewards~U(0,1), paths of 200 steps, "

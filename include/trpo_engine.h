@@ -196,7 +196,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * included; results are bit-identical to eager launches), "tail" (1 = the fused last-layer FVP tail
  * of tail.hip where eligible: f16 split, last hidden width in (128, 256], 17..32 actions), "fused"
  * (whole FVP incl. weight gradients in one launch of fused.hip for one or two hidden layers of
- * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups, the default),
+ * width <= 64, obs <= 128, <= 32 actions: 0 off, 1 = 8-wave workgroups, 2 = 4-wave workgroups, 3 = the
+ * default: two hidden layers of width 49..64 on the scaled f16 hi+lo split (fused16.hip, needs "split_f16"),
+ * other eligible shapes as 2),
  * "low_seg" (f16 split GEMMs with two K-segments: a segment whose running-max product scale lies at
  * least this many binades below the other's -- the O(eps) KL_ff plain-delta terms -- runs on one
  * f16 product instead of three; 4 more binades when the dominant segment has an operand without a

@@ -1,7 +1,7 @@
 """The whole update at the full sizes of BASELINE's other GPU configs against its float64 evaluation
 (oracle/chunked_f64.py in a child process, tests/bign_truth.py): discount + standardise + pg + 10 CG + shs + line
 search, trpo_inksci.py:102-158. C2 (50k states, obs 11, 64x64, 3 actions) and C3 (1M states, obs 128, 64x64,
-18 actions) run the fused FVP on the exact bf16 hi+mid+lo split; C5 (4M states, obs 376, 1024x1024, 17 actions,
+18 actions) run the one-launch FVP on the scaled f16 hi+lo split (fused16.hip); C5 (4M states, obs 376, 1024x1024, 17 actions,
 one GPU) the f16x3 split row GEMMs. C4 is tests/test_gpu_bigN.py."""
 import os
 import subprocess

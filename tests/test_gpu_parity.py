@@ -278,6 +278,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"split_f16": 0, "chain": 2}, {"chain": 2, "split_wg": 1},
     {"split_min_k": 64}, {"split_min_k": 64, "chain": 0},  # few-k row GEMMs on the f32 tile
     {"fused": 0}, {"fused": 1},                               # chain + GEMM weight gradients ; 8-wave fused FVP
+    {"fused": 2}, {"fused": 3, "split_f16": 0},               # bf16 4-wave fused FVP ; the f16 default without f16
     {"low_seg": 0}, {"low_seg": 0, "chain": 0},               # every split segment on three products
     {"planes": 0},                                            # register-staged split instead of the plane kernel
     {"tail": 0}, {"tail": 0, "chain": 0},                     # per-layer last-layer kernels instead of tail.hip
@@ -378,10 +379,14 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
     (128, [64], 32, 63),               # one hidden layer, A = 32, a single partial group
     (16, [16, 48], 17, 1),             # one state
     (128, [64, 64], 18, 100_000),      # many groups per persistent workgroup
+    (128, [64, 64], 3, 4099),          # f16 form: 8 obs tiles, one head tile
+    (40, [64, 49], 32, 777),           # f16 form: 4 obs tiles, a partial hidden tile, A = 32
+    (20, [56, 64], 17, 300),           # f16 form: 2 obs tiles
 ])
 def test_fused_fvp_vs_oracle(gpu_available, obs, hidden, A, n):
-    """The one-launch FVP (fused.hip, both workgroup forms) against the float64 oracle and against
-    the chain + weight-gradient GEMM path it replaces (trpo_inksci.py:56-70)."""
+    """The one-launch FVP (fused.hip, both workgroup forms; fused16.hip on the f16 split where it applies,
+    mode 3) against the float64 oracle and against the chain + weight-gradient GEMM path it replaces
+    (trpo_inksci.py:56-70)."""
     from trpo_amd import Engine
     from trpo_amd._lib import get_option, set_option
     spec = O.PolicySpec(obs, hidden, A)
@@ -391,7 +396,7 @@ def test_fused_fvp_vs_oracle(gpu_available, obs, hidden, A, n):
     saved = get_option("fused")
     out = {}
     try:
-        for mode in (1, 2, 0):
+        for mode in (1, 2, 3, 0):
             set_option("fused", mode)
             e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
             e.set_flat(dd["theta"])
@@ -401,7 +406,7 @@ def test_fused_fvp_vs_oracle(gpu_available, obs, hidden, A, n):
             e.close()
     finally:
         set_option("fused", saved)
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         assert_vec_close(out[mode], ref, REL, f"fused({mode}) Hv {obs} {hidden} {A} n={n}")
         assert_vec_close(out[mode], out[0], REL, f"fused({mode}) vs chain Hv {obs} {hidden} {A} n={n}")
         assert np.array_equal(out[mode], out[(mode, "again")]), "fused FVP is not deterministic"

@@ -1,5 +1,6 @@
-// Device helpers shared by the fused FVP chain (chain.hip) and the fused small-width FVP
-// (fused.hip): the exact bf16 three-way split and the layout of the chain's weight images.
+// Device helpers shared by the fused FVP chain (chain.hip) and the fused small-width FVPs
+// (fused.hip, fused16.hip): the exact bf16 three-way split, the layout of the chain's weight images
+// and of the gradient-pass images.
 #pragma once
 #include "common.h"
 
@@ -9,6 +10,8 @@ typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short cu16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short cu16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+typedef short fs4 __attribute__((ext_vector_type(4)));   // ds_read_b64_tr_b16 results
+typedef short fs8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ unsigned short cb_bits(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
 __device__ __forceinline__ float cb_val(unsigned short b) { return __builtin_bit_cast(float, (unsigned)b << 16); }
@@ -21,6 +24,14 @@ __device__ __forceinline__ void csplit(float x, unsigned short& h, unsigned shor
   const float r2 = r1 - cb_val(m);
   l = cb_bits(r2);
 }
+
+// Gradient-pass images of the fused FVPs (fused.hip, fused16.hip): [state][kFI features] 16-bit planes.
+constexpr int kFI = 64;   // features per image row (one pass operand: up to 4 tiles of 16)
+
+// 32-B chunk (one 16-feature tile) of image row r: tile ^ fswz(r).  The 8 rows a half-wave's
+// transposed read touches (r0 + {0..3, 8..11}) then cover all 64 banks once.
+__device__ __forceinline__ int fswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+__device__ __forceinline__ int fimg(int r, int f) { return r * kFI + ((((f >> 4) ^ fswz(r))) << 4) + (f & 15); }
 
 // 16-B chunk position of k-group g in image row o: g ^ chain_hsw(o).  Makes the
 // 16-lane groups of a ds_read_b128 (MI355X_MICROARCH.md, LDS table) hit 16

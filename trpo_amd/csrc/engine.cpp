@@ -172,6 +172,15 @@ struct trpo_engine {
   // whole FVP (R-forward, head, R-backward and weight gradients) in one launch (fused.hip): one or
   // two hidden layers of width <= 64, obs <= 128, <= 32 actions; reuses the chain's weight images
   bool use_fused() const { return g_options.fused != 0 && chain_otm > 0 && fused_fvp_eligible(L, w.data()); }
+  // the same launch on the f16 split (fused16.hip, option fused = 3): two hidden layers of width 49..64; its
+  // own weight images (2 f16 planes, one scale exponent per job in f16_e) and chunk table
+  uint16_t* f16_img = nullptr;
+  int* f16_tab = nullptr;
+  int* f16_e = nullptr;
+  int f16_nchunks = 0;
+  bool f16_w_valid = false;     // theta parts of the f16 images match theta
+  ChainImgArgs f16_jobs{};
+  bool use_fused16() const { return g_options.fused == 3 && f16 && f16_img && fused16_eligible(L, w.data()); }
   // layer 1's R-backward (and the policy gradient's backward into layer 0) fused with layer 0's weight
   // gradient (rbwd0.hip): f16 split with X's planes, obs <= 128, first hidden width <= 256
   bool use_rbwd0() const {
@@ -421,6 +430,7 @@ struct trpo_engine {
     HIPCHECK(hipHostMalloc((void**)&hsc, sizeof(UpdScalars), hipHostMallocDefault));
     std::memset(hsc, 0, sizeof(UpdScalars));
     setup_chain();
+    setup_fused16();
     HIPCHECK(hipStreamSynchronize(stream));
   }
 
@@ -475,6 +485,53 @@ struct trpo_engine {
     HIPCHECK(hipStreamSynchronize(stream));   // `tab` is a local vector
     chain_nchunks = (int)(tab.size() / 2);
     chain_otm = otm;
+  }
+
+  // fused16.hip's images: the chain's job order with 2 f16 planes per chunk and V_0 padded to
+  // fused16_obs_chunks(obs) chunks
+  void setup_fused16() {
+    if (!fused16_eligible(L, w.data())) return;
+    std::vector<int> tab;
+    int64_t off16 = 0;
+    int nj = 0;
+    auto seg = [&](int l, int trans, int which) {
+      const int K = trans ? w[l + 1] : w[l], O = trans ? w[l] : w[l + 1];
+      const int kc = l == 0 ? fused16_obs_chunks(w[0]) : (K + 31) / 32, otp = (O + 15) / 16 * 16, csz = otp * 8;
+      ChainImgJob& j = f16_jobs.job[nj++];
+      j.src_off = offW[l];
+      j.dst_off = off16 * 8;
+      j.K = K;
+      j.O = O;
+      j.ldw = w[l + 1];
+      j.trans = trans;
+      j.kc = kc;
+      j.otp = otp;
+      j.which = which;
+      j.pad = 0;
+      for (int c = 0; c < kc; ++c) {
+        tab.push_back((int)(off16 + (int64_t)c * csz));
+        tab.push_back(csz);
+      }
+      off16 += (int64_t)kc * csz;
+    };
+    seg(0, 0, 1);
+    for (int l = 1; l < L; ++l) {
+      seg(l, 0, 0);
+      seg(l, 0, 1);
+    }
+    for (int l = L - 1; l >= 1; --l) {
+      seg(l, 1, 0);
+      seg(l, 1, 1);
+    }
+    REQUIRE(nj == kFused16Jobs, "fused16: job count");
+    f16_jobs.n = nj;
+    f16_img = dalloc<uint16_t>((size_t)off16 * 8);
+    f16_tab = dalloc<int>(tab.size());
+    f16_e = dalloc<int>(kFused16Jobs);
+    f16_jobs.img = f16_img;
+    HIPCHECK(hipMemcpyAsync(f16_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));   // `tab` is a local vector
+    f16_nchunks = (int)(tab.size() / 2);
   }
 
   PolicyShape policy_shape() const {
@@ -916,6 +973,7 @@ struct trpo_engine {
     launch_pack(pa, theta, 0, nullptr, stream);
     w3_valid = false;
     chain_w_valid = false;
+    f16_w_valid = false;
     ensure_w3();
     am_reset(am_d(0), L);
     am_reset(am_ds(L - 1), 1);
@@ -1100,6 +1158,10 @@ struct trpo_engine {
     if (prepared && e_top_needed() && !prep_e_top) prepared = false;
     prepare();
     ds_ready = false;   // the FVP's R-backward writes RD (DS_{L-2}'s scratch)
+    if (use_fused16()) {
+      fvp_fused16(v, out, skip);
+      return;
+    }
     if (use_fused()) {
       fvp_fused(v, out, skip);
       return;
@@ -1321,7 +1383,7 @@ struct trpo_engine {
       launch_chain_img(chain_jobs, theta, v, 1, skip, stream);
       check_launch();
     }
-    const int variant = g_options.fused == 2 ? 2 : 1;
+    const int variant = g_options.fused == 1 ? 1 : 2;   // 3 (f16) where fused16.hip does not apply: 4 waves
     const int rb = fused_fvp_states_per_group(variant);
     FusedArgs fa{};
     fa.c = chain_args(v, skip);
@@ -1336,6 +1398,48 @@ struct trpo_engine {
     {
       Scope sp(this, "fvp_fused");
       launch_fvp_fused(fa, grid, variant, stream);
+      check_launch();
+    }
+    {
+      Scope sp(this, "reduce");
+      launch_reduce_slab(slab, grid, slab_stride, P, out, skip, stream);
+      check_launch();
+    }
+    allreduce_f32(out, (size_t)P);
+  }
+
+  // the whole Hv in one launch on the f16 split (fused16.hip) + the slab reduction
+  void fvp_fused16(const float* v, float* out, const int* skip) {
+    if (!f16_w_valid) {
+      Scope sp(this, "fvp_img_w");
+      launch_fused16_img(f16_jobs, theta, v, 0, nullptr, f16_e, stream);
+      check_launch();
+      f16_w_valid = true;
+    }
+    {
+      Scope sp(this, "fvp_img_v");
+      launch_fused16_img(f16_jobs, theta, v, 1, skip, f16_e, stream);
+      check_launch();
+    }
+    const int rb = fused16_states_per_group();
+    Fused16Args fa{};
+    fa.f.c = chain_args(v, skip);
+    fa.f.c.img = f16_img;
+    fa.f.c.tab = f16_tab;
+    fa.f.c.nchunks = f16_nchunks;
+    fa.f.slab = slab;
+    fa.f.slab_stride = slab_stride;
+    for (int l = 0; l < L; ++l) fa.f.offW[l] = offW[l];
+    fa.f.ngroups = (int)((n + rb - 1) / rb);
+    fa.img_e = f16_e;
+    fa.am_x = am_x();
+    fa.am_d1 = am_d(1);
+    fa.am_d2 = am_d(2);
+    const int grid = (int)std::max<int64_t>(
+        1, std::min<int64_t>({(int64_t)fa.f.ngroups, (int64_t)S, (int64_t)num_cus * fused16_groups_per_cu()}));
+    {
+      Scope sp(this, "fvp_fused");
+      launch_fvp_fused16(fa, grid, stream);
       check_launch();
     }
     {
@@ -1544,7 +1648,7 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready, d1_plane, d1_tiled;
+    bool prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready, d1_plane, d1_tiled;
   } upd_flags{};
   void drop_graph() {
     if (upd_exec) {
@@ -1570,6 +1674,7 @@ struct trpo_engine {
       prepared = upd_flags.prepared;
       w3_valid = upd_flags.w3_valid;
       chain_w_valid = upd_flags.chain_w_valid;
+      f16_w_valid = upd_flags.f16_w_valid;
       have_returns = upd_flags.have_returns;
       prep_e_top = upd_flags.prep_e_top;
       ds_ready = upd_flags.ds_ready;
@@ -1609,8 +1714,8 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, have_returns, prep_e_top, ds_ready, d1_plane,
-                            d1_tiled};
+    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready,
+                            d1_plane, d1_tiled};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;

@@ -39,16 +39,6 @@
 namespace trpo {
 namespace {
 
-typedef short fs4 __attribute__((ext_vector_type(4)));
-typedef short fs8 __attribute__((ext_vector_type(8)));
-
-constexpr int kFI = 64;   // features per image row (one pass operand: up to 4 tiles of 16)
-
-// 32-B chunk (one 16-feature tile) of image row r: tile ^ fswz(r).  The 8 rows a half-wave's
-// transposed read touches (r0 + {0..3, 8..11}) then cover all 64 banks once.
-__device__ __forceinline__ int fswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
-__device__ __forceinline__ int fimg(int r, int f) { return r * kFI + ((((f >> 4) ^ fswz(r))) << 4) + (f & 15); }
-
 // NL = layers (2: one hidden layer, 3: two), FW = waves per workgroup, OBC = 64-wide chunks of obs
 #ifndef FUSED_LB
 #define FUSED_LB 2   // workgroups per CU the register budget is sized for (A/B builds: 1)

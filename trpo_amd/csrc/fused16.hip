@@ -1,0 +1,714 @@
+// Fused small-width Fisher-vector product on the f16 split (gfx950 / CDNA4).
+//
+// The whole FVP of trpo_inksci.py:56-70 (Pearlmutter's R-operator) for a policy
+// with two tanh hidden layers of width 49..64, obs <= 128 and <= 32 actions (C2, C3) in one persistent
+// launch per shard, structured as fused.hip (16 states per wave through the R-forward, the R-softmax head
+// and the R-backward in MFMA accumulator layout; per-group weight-gradient passes over two LDS images;
+// one slab per workgroup) with three differences:
+//
+//  * Arithmetic.  Every product runs on v_mfma_f32_16x16x32_f16 with each f32 operand scaled by a power of
+//    two and split into f16 hi + lo (3 products, 2^-21 relative per operand; gemm.hip rowgemm3 / tail.hip),
+//    where fused.hip takes 6 bf16 products.  Half the MFMAs, 2/3 of the image and weight-chunk bytes.
+//  * Scales.  Weights: one exponent per image job, set by the image builder from the job's max |w|.
+//    X, D_1, D_2: the engine's running-max slots.  H: fixed (|tanh| <= 1).  Values produced in the launch
+//    (RH_1, RH_2, the head's RD, RD_1, RD_0) take a per-state exponent as B operands of the chain steps (the
+//    max over the state's features: 4 lanes) and a per-group exponent in the gradient-pass images, whose
+//    k dimension runs over states (the wave maxima meet in LDS behind a barrier the pass has anyway).
+//    A chain step's two segments carry different scales: the accumulator is rescaled by the power of two
+//    between them, and every accumulator is unscaled to true f32 values before it is used or summed.
+//  * Shapes are compile-time (hidden tiles 4, obs tiles TI0, head tiles OTA): no runtime-width branches.
+//    Weight chunks stream through two LDS buffers (one barrier per chunk); the next group's first chunk
+//    and first X chunk are loaded during the current group's last pass.
+//
+// States past the shard end read zeros (buffer descriptors): their D / RD and contributions are exactly 0.
+#include "chain_common.h"
+#include "rowepi.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <type_traits>
+
+#ifndef FUSED16_FW
+#define FUSED16_FW 4   // waves per workgroup (16 states each)
+#endif
+#ifndef FUSED16_LB
+#define FUSED16_LB 2   // workgroups per CU the register budget is sized for
+#endif
+
+
+namespace trpo {
+namespace {
+
+typedef _Float16 fh8 __attribute__((ext_vector_type(8)));
+typedef __fp16 fp16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned cu32x2 __attribute__((ext_vector_type(2)));
+
+// (a, b) * 1 -> packed f16 hi pair and lo pair, round toward zero: a - hi is exact in f32 and below
+// ulp16(a), so hi + lo is within 2^-21 |a| (tail.hip split8)
+// (returned as {hi pair, lo pair})
+__device__ __forceinline__ cu32x2 split2(float a, float b) {
+  const fp16x2 hp = __builtin_amdgcn_cvt_pkrtz(a, b);
+  const fp16x2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], b - (float)hp[1]);
+  return cu32x2{__builtin_bit_cast(unsigned, hp), __builtin_bit_cast(unsigned, lp)};
+}
+
+// B operand (hi, lo) of v_mfma_f32_16x16x32_f16 from two acc-layout tiles times s (chain_mkb's k order)
+__device__ __forceinline__ void mkb16(const f32x4& x0, const f32x4& x1, float s, fh8 (&b)[2]) {
+  const cu32x2 p0 = split2(x0[0] * s, x0[1] * s), p1 = split2(x0[2] * s, x0[3] * s);
+  const cu32x2 p2 = split2(x1[0] * s, x1[1] * s), p3 = split2(x1[2] * s, x1[3] * s);
+  const cu32x4 H = {p0[0], p1[0], p2[0], p3[0]}, L = {p0[1], p1[1], p2[1], p3[1]};
+  b[0] = __builtin_bit_cast(fh8, H);
+  b[1] = __builtin_bit_cast(fh8, L);
+}
+
+// c += a b over the split: al bh + ah bl + ah bh, smallest terms first
+__device__ __forceinline__ f32x4 mfma3(const fh8 (&a)[2], const fh8 (&b)[2], f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ f32x4 ldexp4(const f32x4& x, int e) {
+  f32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = __builtin_amdgcn_ldexpf(x[i], e);
+  return r;
+}
+
+// max |x| over the first N acc-layout tiles of this lane, then over the 4 lanes of the same state
+// (l, l^16, l^32, l^48): the state's max over all its features, on every one of its lanes
+template <int N>
+__device__ __forceinline__ float state_max(const f32x4 (&x)[4]) {
+  float m = 0.0f;
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m = fmaxf(m, fabsf(x[t][j]));
+  return xmax_f<false>(xmax_f<true>(m));
+}
+
+// max over the 16 lanes of a row (DPP; every lane of the row ends with it)
+__device__ __forceinline__ float max16_dpp(float v) {
+  v = fmaxf(v, dpp_f<kDppX1>(v));
+  v = fmaxf(v, dpp_f<kDppX2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  return fmaxf(v, dpp_f<kDppMirror>(v));
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// weight images: the chain's layout (chain.hip chain_img_kernel) with 2 f16 planes, scaled per job.  Every
+// block of a job takes the job's max |w| itself (<= 128 x 64 values), so one launch does it all.
+// ---------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, const float* theta, const float* v,
+                                                          int which, const int* skip, int* img_e) {
+  __shared__ float red[4];
+  if (skip && *skip) return;
+  const ChainImgJob& j = a.job[blockIdx.y];
+  if (j.which != which) return;
+  const float* src = (which ? v : theta) + j.src_off;
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < j.K * j.O; i += 256) m = fmaxf(m, fabsf(src[i]));   // W_l is K x O or O x K, dense
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = f16_scale_exp(m);
+  if (blockIdx.x == 0 && threadIdx.x == 0) img_e[blockIdx.y] = e;
+  const float sc = __builtin_ldexpf(1.0f, e);
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= j.kc * j.otp * 4) return;
+  const int gg = idx & 3;
+  const int o = (idx >> 2) % j.otp;
+  const int c = (idx >> 2) / j.otp;
+  float x[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = 32 * c + chain_perm(8 * gg + q);
+    x[q] = 0.0f;
+    if (o < j.O && k < j.K) x[q] = (j.trans ? src[(size_t)o * j.ldw + k] : src[(size_t)k * j.ldw + o]) * sc;
+  }
+  cu32x4 H, L;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const cu32x2 p = split2(x[2 * i], x[2 * i + 1]);
+    H[i] = p[0];
+    L[i] = p[1];
+  }
+  unsigned short* dst = a.img + j.dst_off + (size_t)c * 2 * j.otp * 32 + o * 32 + ((gg ^ chain_hsw(o)) << 3);
+  *reinterpret_cast<cu32x4*>(dst) = H;
+  *reinterpret_cast<cu32x4*>(dst + (size_t)j.otp * 32) = L;
+}
+
+// image jobs (kernels.h, kFused16Jobs)
+enum { jV0 = 0, jW1, jV1, jW2, jV2, jW2t, jV2t, jW1t, jV1t };
+
+// FW = waves per workgroup, TI0 = 16-feature tiles of obs (1, 2, 4, 8), OTA = 16-action tiles of the head
+template <int FW, int LB, int TI0, int OTA>
+__global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16Args fa) {
+  constexpr int OTM = 4;                       // 16-feature tiles of a hidden layer
+  constexpr int NT = FW * 64;
+  constexpr int CHU = 8 * 16 * OTM;            // 16-B units of a 64-row chunk: 2 planes x 64 rows x 64 B
+  constexpr int NLD = (CHU + NT - 1) / NT;
+  constexpr int RB = 16 * FW;                  // states per group
+  constexpr int PL = RB * kFI;                 // u16 per image plane
+  constexpr int KS = RB / 32;                  // k-steps of a gradient pass
+  constexpr int KX = (TI0 + 1) / 2;            // 32-deep chunks of obs
+  constexpr int OBC = (TI0 + 3) / 4;           // 64-feature X passes
+  constexpr int TW0 = (TI0 * OTM + FW - 1) / FW;   // owned gradient tiles: obs x hidden
+  constexpr int TWH = (OTM * OTM + FW - 1) / FW;   //                       hidden x hidden
+  constexpr int TWL = (OTM * OTA + FW - 1) / FW;   //                       hidden x actions
+  constexpr int RING = 2;
+  __shared__ cu32x4 wl[2][CHU];
+  __shared__ __attribute__((aligned(16))) unsigned short simg[2][2 * PL];   // [act | delta] images, hi / lo planes
+  __shared__ float sb[FW][3][64];                                          // per-wave bias sums
+  __shared__ __attribute__((aligned(16))) float sc[3][64];                // the tangent's biases c_l
+  __shared__ float sred[5][FW];                                            // wave maxima: RH1 RH2 RDh RD1 RD0
+
+  const ChainArgs& a = fa.f.c;
+  if (a.skip && *a.skip) return;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  unsigned short* const sA = &simg[0][0];
+  unsigned short* const sD = &simg[1][0];
+
+  for (int i = threadIdx.x; i < FW * 3 * 64; i += NT) (&sb[0][0][0])[i] = 0.0f;
+  for (int i = threadIdx.x; i < 3 * 64; i += NT) {
+    const int l = i >> 6, j = i & 63;
+    sc[l][j] = j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
+  }
+
+  // scale exponents (wave-uniform)
+  const int eX = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_x));
+  const int eD1 = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_d1));
+  const int eD2 = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_d2));
+  const int eH = f16_scale_exp(1.0f);
+  int ej[kFused16Jobs];
+#pragma unroll
+  for (int i = 0; i < kFused16Jobs; ++i) ej[i] = __builtin_amdgcn_readfirstlane(fa.img_e[i]);
+  const float sX = __builtin_ldexpf(1.0f, eX), sH = __builtin_ldexpf(1.0f, eH);
+  const float sD1 = __builtin_ldexpf(1.0f, eD1), sD2 = __builtin_ldexpf(1.0f, eD2);
+
+  f32x4 dw0[TW0], dwh[TWH], dwl[TWL];
+#pragma unroll
+  for (int k = 0; k < TW0; ++k) dw0[k] = z4;
+#pragma unroll
+  for (int k = 0; k < TWH; ++k) dwh[k] = z4;
+#pragma unroll
+  for (int k = 0; k < TWL; ++k) dwl[k] = z4;
+
+  f32x4 acc[OTM], S[OTM], PF[OTM], RH1[OTM], RH2[OTM];
+  // H_2 and H_1 in f32 for the R-backward epilogues' (1 - H^2): the images' hi + lo (22 bits) is not exact, and
+  // near saturation 1 - H^2 is as small as H's own rounding
+  f32x4 H2f[OTM], H1f[OTM];
+  f32x4 xn0 = z4, xn1 = z4;   // first X chunk of the next group (loaded one group ahead)
+  const cu32x4* img = reinterpret_cast<const cu32x4*>(a.img);
+  cu32x4 wr[NLD];             // the next weight chunk (loaded one chunk ahead, across groups too)
+  auto gload = [&](int qq) {
+    qq = qq < a.nchunks ? qq : 0;   // past the last chunk: the next group's first
+    const int off = a.tab[2 * qq], sz = a.tab[2 * qq + 1];
+    const cu32x4* src = img + off;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      wr[i] = src[idx < sz ? idx : sz - 1];
+    }
+  };
+  gload(0);
+
+  const int ngroups = fa.f.ngroups;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t row_b = (int64_t)grp * RB;
+    const int rb = (int)((int64_t)a.n - row_b < RB ? (int64_t)a.n - row_b : RB);
+    // lane-derived offsets are recomputed per group from an opaque copy of threadIdx.x (hoisted out of the
+    // group loop they would stay live across the whole launch)
+    int tid;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+    const int lane = tid & 63, g = lane >> 4, s = lane & 15;
+    const int lrow = wave * 16 + s;
+    const int frag = s * 32 + ((g ^ chain_hsw(s)) << 3);
+
+    // ---- weight-chunk stream: chunk q goes to buffer q & 1, one barrier per chunk ----
+    int q = 0;
+    const unsigned short* W = nullptr;   // this lane's A fragment in the current chunk
+    auto chunk_begin = [&]() __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_barrier(0);
+      cu32x4* buf = &wl[q & 1][0];
+#pragma unroll
+      for (int i = 0; i < NLD; ++i) {
+        const int idx = threadIdx.x + i * NT;
+        if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[i];
+      }
+      lds_barrier();   // chunk q visible; every wave is past chunk q - 1, so buffer (q + 1) & 1 is free
+      gload(q + 1);
+      W = reinterpret_cast<const unsigned short*>(buf) + frag;
+      ++q;
+    };
+
+    // ---- image helpers (planes hi, lo; each image holds values times one power of two) ----
+    auto put4 = [&](unsigned short* slot, int t, const f32x4& x, float m) {
+      const cu32x2 p0 = split2(x[0] * m, x[1] * m), p1 = split2(x[2] * m, x[3] * m);
+      const int o = fimg(lrow, 16 * t + 4 * g);
+      *reinterpret_cast<cu32x2*>(slot + o) = cu32x2{p0[0], p1[0]};
+      *reinterpret_cast<cu32x2*>(slot + PL + o) = cu32x2{p0[1], p1[1]};
+    };
+    auto putb = [&](unsigned short* slot, int c, const fh8 (&b)[2]) {   // a B operand of chunk c
+      const int o0 = fimg(lrow, 32 * c + 4 * g), o1 = fimg(lrow, 32 * c + 16 + 4 * g);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const cu32x4 v = __builtin_bit_cast(cu32x4, b[p]);
+        *reinterpret_cast<cu32x2*>(slot + p * PL + o0) = cu32x2{v[0], v[1]};
+        *reinterpret_cast<cu32x2*>(slot + p * PL + o1) = cu32x2{v[2], v[3]};
+      }
+    };
+    // 16x16x32 operand of feature tile ft, k-step ks: lane (i = lane & 15, g) <- states 32ks + 8g .. +7
+    const int tq = (lane >> 2) & 3, tp = lane & 3;
+    auto tfrag = [&](const unsigned short* slot, int ft, int ks, fh8 (&f)[2]) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        fs8 v;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int r = 32 * ks + 8 * g + 4 * t + tq;
+          const fs4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) fs4*)(slot + p * PL + r * kFI + (((ft ^ fswz(r))) << 4) + 4 * tp));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * t + e] = x[e];
+        }
+        f[p] = __builtin_bit_cast(fh8, v);
+      }
+    };
+    // gradient products of this wave's tiles of a TI x TJ layer whose act tile lies in [ti0, ti0 + 4),
+    // unscaled by 2^-e into the launch-long accumulators
+    auto run = [&](auto& dacc, auto TI_, auto TJ_, int ti0, int e) __attribute__((always_inline)) {
+      constexpr int TI = decltype(TI_)::value, TJ = decltype(TJ_)::value;
+      constexpr int TWm = sizeof(dacc) / sizeof(f32x4);
+#pragma unroll
+      for (int k = 0; k < TWm; ++k) {
+        const int u = wave + FW * k;
+        const int it = u / TJ, jt = u % TJ;
+        if (u < TI * TJ && it >= ti0 && it < ti0 + 4) {
+          f32x4 c = z4;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            fh8 fa_[2], fd_[2];
+            tfrag(sA, it - ti0, ks, fa_);
+            tfrag(sD, jt, ks, fd_);
+            c = mfma3(fa_, fd_, c);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dacc[k][i] = __builtin_fmaf(c[i], __builtin_amdgcn_ldexpf(1.0f, -e), dacc[k][i]);
+        }
+      }
+    };
+    // bias sums of layer m from acc-layout RD tiles: sum over the wave's 16 states
+    auto bias_add = [&](int m, auto OT_, const f32x4 (&R)[OTM]) {
+      constexpr int OT = decltype(OT_)::value;
+#pragma unroll
+      for (int t = 0; t < OT; ++t) {
+        f32x4 v = R[t];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = sum16_dpp(v[j]);
+        if (s == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sb[wave][m][16 * t + 4 * g + j] += v[j];
+        }
+      }
+    };
+    // this wave's max of a tensor whose per-state maxima are m -> sred[k][wave]; its group exponent
+    auto wave_max = [&](int k, float m) {
+      m = max16_dpp(m);
+      if (lane == 0) sred[k][wave] = m;
+    };
+    auto group_exp = [&](int k) {
+      float m = sred[k][0];
+#pragma unroll
+      for (int w = 1; w < FW; ++w) m = fmaxf(m, sred[k][w]);
+      return __builtin_amdgcn_readfirstlane(f16_scale_exp(m));
+    };
+
+    auto rsrc = [&](const float* p, int ld) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(p + row_b * ld), 0, rb * ld * 4, 0x00020000);
+    };
+    auto voff = [&](int ld, int t) {
+      const int col = 16 * t + 4 * g;
+      return col < ld ? (lrow * ld + col) * 4 : rb * ld * 4;
+    };
+    auto ld4 = [&](__amdgpu_buffer_rsrc_t r, int vo) -> f32x4 {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0));
+    };
+    auto bias4 = [&](int l, int t) -> f32x4 { return *reinterpret_cast<const f32x4*>(&sc[l][16 * t + 4 * g]); };
+
+    auto mma = [&](auto OT_, const fh8 (&b)[2]) __attribute__((always_inline)) {
+      constexpr int OT = decltype(OT_)::value;
+      constexpr int pl = OT * 512;   // u16 per plane of the chunk
+      fh8 f[2], nx[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const fh8*>(W + p * pl);
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) {
+        if (ot + 1 < OT) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) nx[p] = *reinterpret_cast<const fh8*>(W + p * pl + (ot + 1) * 512);
+        }
+        acc[ot] = mfma3(f, b, acc[ot]);
+        if (ot + 1 < OT) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) f[p] = nx[p];
+        }
+      }
+    };
+
+    // One chain step: acc = [S (KC0 chunks, registers, times 2^eS per state) x job jS |
+    //                        M1 (KC1 chunks, memory, times sM) x job jS + 1], unscaled to f32 on return;
+    // the epilogue operand Pre is prefetched into PF; cap (optional) receives M1's split planes.
+    auto step = [&](auto OT_, auto KC0_, auto KC1_, int jS, int eS, const float* M1, int ld1, float sM, int eM,
+                    const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre) __attribute__((always_inline)) {
+      constexpr int OT = decltype(OT_)::value, KC0 = decltype(KC0_)::value, KC1 = decltype(KC1_)::value;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) acc[t] = z4;
+      const __amdgpu_buffer_rsrc_t r1 = rsrc(M1, ld1);
+      const int oob1 = rb * ld1 * 4;
+      auto mld = [&](int cc, int h) { return ld4(r1, cc < KC1 ? voff(ld1, 2 * cc + h) : oob1); };
+      f32x4 n0 = z4, n1 = z4, m0 = z4, m1 = z4;
+      if (pre) {
+        n0 = xn0;
+        n1 = xn1;
+      } else if (KC0 < RING) {
+        n0 = mld(0, 0);
+        n1 = mld(0, 1);
+      }
+      if constexpr (KC0 == 0) {
+        m0 = mld(1, 0);
+        m1 = mld(1, 1);
+      }
+      if constexpr (KC0 > 0) {
+        const float sS = __builtin_amdgcn_ldexpf(1.0f, eS);
+#pragma unroll
+        for (int c = 0; c < KC0; ++c) {
+          fh8 b[2];
+          mkb16(S[2 * c], S[2 * c + 1], sS, b);
+          chunk_begin();
+          if (c == KC0 - RING) {
+            n0 = mld(0, 0);
+            n1 = mld(0, 1);
+          }
+          if (c == KC0 - 1) {
+            m0 = mld(1, 0);
+            m1 = mld(1, 1);
+          }
+          mma(OT_, b);
+        }
+        // segment scales: 2^(ej[jS] + eS) -> 2^(ej[jS + 1] + eM)
+        const int d = ej[jS + 1] + eM - ej[jS] - eS;
+#pragma unroll
+        for (int t = 0; t < OT; ++t) acc[t] = ldexp4(acc[t], d);
+      }
+      const int jM = KC0 > 0 ? jS + 1 : jS;
+#pragma unroll
+      for (int c = 0; c < KC1; ++c) {
+        const f32x4 x0 = n0, x1 = n1;
+        n0 = m0;
+        n1 = m1;
+        chunk_begin();
+        m0 = mld(c + RING, 0);
+        m1 = mld(c + RING, 1);
+        if (c == 0) {
+          const __amdgpu_buffer_rsrc_t rp = rsrc(Pre, ldp);
+#pragma unroll
+          for (int t = 0; t < OTM; ++t) PF[t] = ld4(rp, t < OTp ? voff(ldp, t) : rb * ldp * 4);
+        }
+        fh8 b[2];
+        mkb16(x0, x1, sM, b);
+        if (cap) putb(cap, c, b);
+        mma(OT_, b);
+      }
+      const int eu = -(ej[jM] + eM);
+#pragma unroll
+      for (int t = 0; t < OT; ++t) acc[t] = ldexp4(acc[t], eu);
+    };
+
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    using C4 = std::integral_constant<int, OTM>;
+    using COTA = std::integral_constant<int, OTA>;
+    using CKX = std::integral_constant<int, KX>;
+    using C0 = std::integral_constant<int, 0>;
+
+    if (grp == (int)blockIdx.x) {   // later groups' first X chunk is loaded during the previous group
+      const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
+      xn0 = ld4(rx, voff(a.ld[0], 0));
+      xn1 = ld4(rx, voff(a.ld[0], 1));
+    }
+
+    // ---- R-forward: RH_1 = (1 - H_1^2)(X V_0 + c_0) ----
+    step(C4{}, C0{}, CKX{}, jV0, 0, a.X, a.ld[0], sX, eX, a.H[1], a.ld[1], OTM, nullptr, true);
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 cb = bias4(0, t), h = PF[t];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) RH1[t][i] = c_one_minus_sq(h[i]) * (acc[t][i] + cb[i]);
+    }
+    float mst = state_max<OTM>(RH1);
+    wave_max(0, mst);
+    // ---- RH_2 = (1 - H_2^2)(RH_1 W_1 + H_1 V_1 + c_1) ----
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) S[t] = RH1[t];
+    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false);
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 cb = bias4(1, t), h = PF[t];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) RH2[t][i] = c_one_minus_sq(h[i]) * (acc[t][i] + cb[i]);
+      H2f[t] = h;
+    }
+    mst = state_max<OTM>(RH2);
+    wave_max(1, mst);
+
+    // ---- R-softmax head; H_2 captured into the act image ----
+    {
+      const int A = a.w[3];
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) S[t] = RH2[t];
+      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false);
+      // f64 as chain.hip / fused.hip, bit for bit on the same z and p
+      float zf[8], pf[8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 cb = bias4(2, t);
+        const f32x4 pv = PF[t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool real = 16 * t + 4 * g + i < A;
+          zf[4 * t + i] = real ? acc[t][i] + cb[i] : 0.0f;
+          pf[4 * t + i] = real ? pv[i] : 0.0f;
+        }
+      }
+      double prz = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) prz += (double)pf[k] * (double)zf[k];
+      prz = sum4lanes(prz);
+      double spB = 0.0, sRAB = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool real = 16 * (k >> 2) + 4 * g + (k & 3) < A;
+        const double pd = (double)pf[k];
+        const double Rp = pd * ((double)zf[k] - prz);
+        const double den = pd + (double)kEps;
+        const double Aa = real ? pd / den : 0.0;
+        const double B = real ? (double)kEps / den : 0.0;
+        spB += pd * B;
+        sRAB += Rp * Aa * B;
+      }
+      spB = sum4lanes(spB);
+      sRAB = sum4lanes(sRAB);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * t + i;
+          const bool real = 16 * t + 4 * g + i < A;
+          const double pd = (double)pf[k];
+          const double Rp = pd * ((double)zf[k] - prz);
+          const double den = pd + (double)kEps;
+          const double Aa = real ? pd / den : 0.0;
+          const double B = real ? (double)kEps / den : 0.0;
+          const double rd = a.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
+          r[i] = real ? (float)rd : 0.0f;
+        }
+        S[t] = r;
+      }
+#pragma unroll
+      for (int t = 2; t < OTM; ++t) S[t] = z4;
+      mst = state_max<2>(S);
+      wave_max(2, mst);
+      // gradient pass: (Hv)_W_2 += H_2^T RD_2  (act captured in the step)
+      lds_barrier();
+      const int eg = group_exp(2);
+      const float sg = __builtin_ldexpf(1.0f, eg);
+#pragma unroll
+      for (int t = 0; t < OTA; ++t) put4(sD, t, S[t], sg);
+      bias_add(2, COTA{}, S);
+      lds_barrier();
+      run(dwl, C4{}, COTA{}, 0, eH + eg);
+    }
+
+    // ---- R-backward into layer 2's input: RD_1 = (RD_2 W_2^T + D_2 V_2^T)(1 - H_2^2) + E_1 RH_2; D_2 captured ----
+    step(C4{}, C1{}, C1{}, jW2t, f16_scale_exp(mst), a.D[2], a.ld[3], sD2, eD2, a.E[1], a.ld[2], OTM, sD, false);
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 h = H2f[t], e = PF[t];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH2[t][i], acc[t][i] * c_one_minus_sq(h[i]));
+    }
+    mst = state_max<OTM>(S);
+    wave_max(3, mst);
+    {
+      // (Hv)_W_2 += RH_2^T D_2 ; H_1 for the next pass is loaded meanwhile
+      lds_barrier();
+      const int eg = group_exp(1);
+      const float sg = __builtin_ldexpf(1.0f, eg);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sA, t, RH2[t], sg);
+      const __amdgpu_buffer_rsrc_t rn = rsrc(a.H[1], a.ld[1]);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) H1f[t] = ld4(rn, voff(a.ld[1], t));
+      lds_barrier();
+      run(dwl, C4{}, COTA{}, 0, eg + eD2);
+      // (Hv)_W_1 += H_1^T RD_1
+      lds_barrier();
+      const int eg1 = group_exp(3);
+      const float sg1 = __builtin_ldexpf(1.0f, eg1);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sD, t, S[t], sg1);
+      bias_add(1, C4{}, S);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sA, t, H1f[t], sH);
+      lds_barrier();
+      run(dwh, C4{}, C4{}, 0, eH + eg1);
+    }
+
+    // ---- R-backward into layer 1's input: RD_0 = (RD_1 W_1^T + D_1 V_1^T)(1 - H_1^2) + E_0 RH_1; D_1 captured ----
+    step(C4{}, C2{}, C2{}, jW1t, f16_scale_exp(mst), a.D[1], a.ld[2], sD1, eD1, a.E[0], a.ld[1], OTM, sD, false);
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 h = H1f[t], e = PF[t];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH1[t][i], acc[t][i] * c_one_minus_sq(h[i]));
+    }
+    mst = state_max<OTM>(S);
+    wave_max(4, mst);
+    {
+      // (Hv)_W_1 += RH_1^T D_1 ; X's first 64 features are loaded meanwhile
+      lds_barrier();
+      const int eg = group_exp(0);
+      const float sg = __builtin_ldexpf(1.0f, eg);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sA, t, RH1[t], sg);
+      f32x4 nxt[OTM];
+      const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], t));
+      lds_barrier();
+      run(dwh, C4{}, C4{}, 0, eg + eD1);
+      // (Hv)_W_0 += X^T RD_0 in 64-feature chunks of X
+      lds_barrier();
+      const int eg0 = group_exp(4);
+      const float sg0 = __builtin_ldexpf(1.0f, eg0);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sD, t, S[t], sg0);
+      bias_add(0, C4{}, S);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) put4(sA, t, nxt[t], sX);
+#pragma unroll
+      for (int ch = 0; ch < OBC; ++ch) {
+        if (ch + 1 < OBC) {
+#pragma unroll
+          for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], 4 * (ch + 1) + t));
+        } else {
+          // the next group's first X chunk, in flight during this last gradient pass
+          const int64_t nb = row_b + (int64_t)gridDim.x * RB;
+          const int nrb = (int)((int64_t)a.n - nb < RB ? (int64_t)a.n - nb : RB);
+          const __amdgpu_buffer_rsrc_t rxn = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(a.X + (nb < a.n ? nb : 0) * a.ld[0]), 0, nb < a.n ? nrb * a.ld[0] * 4 : 0, 0x00020000);
+          xn0 = ld4(rxn, voff(a.ld[0], 0));
+          xn1 = ld4(rxn, voff(a.ld[0], 1));
+        }
+        lds_barrier();
+        run(dw0, std::integral_constant<int, TI0>{}, C4{}, 4 * ch, eX + eg0);
+        if (ch + 1 < OBC) {
+          lds_barrier();
+#pragma unroll
+          for (int t = 0; t < OTM; ++t) put4(sA, t, nxt[t], sX);
+        }
+      }
+    }
+  }
+
+  // ---- this workgroup's slab: owned gradient tiles (C layout: rows 4g + r, column s) and biases ----
+  __syncthreads();
+  const int lane = threadIdx.x & 63, g = lane >> 4, s = lane & 15;
+  float* out = fa.f.slab + (size_t)blockIdx.x * fa.f.slab_stride;
+  auto wout = [&](auto& dacc, int m, int TI, int TJ) __attribute__((always_inline)) {
+    constexpr int TWm = sizeof(dacc) / sizeof(f32x4);
+    const int wi = a.w[m], wj = a.w[m + 1];
+#pragma unroll
+    for (int k = 0; k < TWm; ++k) {
+      const int u = wave + FW * k;
+      if (u < TI * TJ) {
+        const int it = u / TJ, jt = u - (u / TJ) * TJ;
+        const int j = 16 * jt + s;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * it + 4 * g + r;
+          if (i < wi && j < wj) out[fa.f.offW[m] + (int64_t)i * wj + j] = dacc[k][r];
+        }
+      }
+    }
+  };
+  wout(dw0, 0, TI0, OTM);
+  wout(dwh, 1, OTM, OTM);
+  wout(dwl, 2, OTM, OTA);
+  for (int i = threadIdx.x; i < 3 * 64; i += NT) {
+    const int m = i >> 6, j = i & 63;
+    if (j < a.w[m + 1]) {
+      float t = 0.0f;
+#pragma unroll
+      for (int u = 0; u < FW; ++u) t += sb[u][m][j];
+      out[a.offb[m] + j] = t;
+    }
+  }
+}
+
+int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
+
+template <int TI0>
+void launch_ti0(const Fused16Args& a, int grid, hipStream_t s) {
+  constexpr int FW = FUSED16_FW, LB = FUSED16_LB;
+  if (a.f.c.w[3] <= 16)
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1>), dim3(grid), dim3(FW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2>), dim3(grid), dim3(FW * 64), 0, s, a);
+}
+
+}  // namespace
+
+bool fused16_eligible(int L, const int* w) {
+  return L == 3 && w[0] >= 1 && w[0] <= 128 && w[1] > 48 && w[1] <= 64 && w[2] > 48 && w[2] <= 64 && w[3] >= 1 &&
+         w[3] <= 32;
+}
+
+int fused16_obs_chunks(int obs) { return (ti0_of(obs) + 1) / 2; }
+int fused16_states_per_group() { return 16 * FUSED16_FW; }
+int fused16_groups_per_cu() { return FUSED16_LB; }
+
+void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
+                        int* img_e, hipStream_t s) {
+  int maxb = 1;
+  for (int i = 0; i < a.n; ++i) {
+    const ChainImgJob& j = a.job[i];
+    if (j.which == which) maxb = std::max(maxb, (j.kc * j.otp * 4 + 255) / 256);
+  }
+  hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
+}
+
+void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) {
+  if (grid <= 0) return;
+  if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16 fvp: unsupported shape");
+  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16 fvp: chunk table");
+  const int rb = fused16_states_per_group();
+  if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16 fvp: group count does not match");
+  switch (ti0_of(a.f.c.w[0])) {
+    case 1: launch_ti0<1>(a, grid, s); break;
+    case 2: launch_ti0<2>(a, grid, s); break;
+    case 4: launch_ti0<4>(a, grid, s); break;
+    default: launch_ti0<8>(a, grid, s); break;
+  }
+}
+
+}  // namespace trpo

@@ -23,7 +23,8 @@ struct Options {
   int split_min_k; // row GEMMs whose every segment has K < split_min_k stay on f32 MFMA (epilogue-bound)
   int graphs;      // engine: replay the update's sync-free prefix as a captured hipGraph
   int tail;        // engine: fused last-layer FVP tail (tail.hip) where eligible: 0 off, 1 on
-  int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves (default)
+  int fused;       // engine: whole small-width FVP in one launch (fused.hip): 0 off, 1 = 8 waves, 2 = 4 waves,
+                   // 3 (default) = on the f16 split (fused16.hip) where it applies, else 2
   int low_seg;     // f16 split GEMMs: a segment whose product scale sits >= low_seg binades below the other
                    // segment's runs on one product (hi x hi) instead of three; 0 = off (gemm.hip)
   int planes;      // engine: row GEMMs whose operands have pre-split k-blocked f16 planes take the LDS-DMA
@@ -380,6 +381,27 @@ struct FusedArgs {
 bool fused_fvp_eligible(int L, const int* w);
 int fused_fvp_states_per_group(int variant);
 void launch_fvp_fused(const FusedArgs& a, int grid, int variant, hipStream_t s);
+
+// The same one-launch FVP on the f16 split (fused16.hip) for two hidden layers of width 49..64, obs <= 128 and
+// <= 32 actions (C2, C3).  Weight images: the chain's job list (ChainImgJob; kc = fused16_obs_chunks(obs) for
+// V_0) as 32-deep chunks of [2 f16 planes (hi, lo)][otp rows][32], each job scaled by a power of two whose
+// exponent launch_fused16_img writes to img_e[job]; jobs in the order V_0 | W_1 V_1 | W_2 V_2 | W_2^T V_2^T |
+// W_1^T V_1^T.  X, D_1 and D_2 are scaled from the engine's running-max slots.
+constexpr int kFused16Jobs = 9;
+struct Fused16Args {
+  FusedArgs f;                       // f.c.img / f.c.tab / f.c.nchunks: the f16 images and their chunk table
+  const int* img_e;                  // [kFused16Jobs] scale exponents of the images
+  const unsigned* am_x;              // running-max slots: X, D_1, D_2
+  const unsigned* am_d1;
+  const unsigned* am_d2;
+};
+bool fused16_eligible(int L, const int* w);
+int fused16_obs_chunks(int obs);     // 32-deep k-chunks of V_0's image (obs rounded to 32, 64 or 128)
+int fused16_states_per_group();
+int fused16_groups_per_cu();
+void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
+                        int* img_e, hipStream_t s);
+void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
