@@ -100,6 +100,7 @@ __device__ __forceinline__ double xadd_d(double v) {
          __builtin_bit_cast(double, ((unsigned long long)hb << 32) | lb);
 }
 constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+constexpr int kDppRor4 = 0x124, kDppRor8 = 0x128;   // row_ror:4 / row_ror:8 (rotate within a 16-lane row)
 __device__ __forceinline__ float sum16_dpp(float v) {
   v += dpp_f<kDppX1>(v);
   v += dpp_f<kDppX2>(v);

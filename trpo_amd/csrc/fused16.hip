@@ -34,6 +34,11 @@
 #ifndef FUSED16_LB
 #define FUSED16_LB 2   // workgroups per CU the register budget is sized for
 #endif
+// Ablation builds for profiling only (tools/variant.sh; never the shipped library): bit 0 = no per-state
+// activation loads, 1 = no gradient passes, 2 = no weight-chunk loads, 3 = no chunk barriers
+#ifndef FUSED16_ABL
+#define FUSED16_ABL 0
+#endif
 
 
 namespace trpo {
@@ -100,6 +105,7 @@ __device__ __forceinline__ float max16_dpp(float v) {
 // weight images: the chain's layout (chain.hip chain_img_kernel) with 2 f16 planes, scaled per job.  Every
 // block of a job takes the job's max |w| itself (<= 128 x 64 values), so one launch does it all.
 // ---------------------------------------------------------------------------------------------------------
+constexpr int kImgMax = 128 * 64;   // the largest weight matrix of an eligible shape
 __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, const float* theta, const float* v,
                                                           int which, const int* skip, int* img_e) {
   __shared__ float red[4];
@@ -108,7 +114,9 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
   if (j.which != which) return;
   const float* src = (which ? v : theta) + j.src_off;
   float m = 0.0f;
-  for (int i = threadIdx.x; i < j.K * j.O; i += 256) m = fmaxf(m, fabsf(src[i]));   // W_l is K x O or O x K, dense
+  const int last = j.K * j.O - 1;   // W_l is K x O or O x K, dense, at most 128 x 64: 32 loads in flight per lane
+#pragma unroll
+  for (int u = 0; u < kImgMax / 256; ++u) m = fmaxf(m, fabsf(src[min((int)threadIdx.x + 256 * u, last)]));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -204,19 +212,25 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // near saturation 1 - H^2 is as small as H's own rounding
   f32x4 H2f[OTM], H1f[OTM];
   f32x4 xn0 = z4, xn1 = z4;   // first X chunk of the next group (loaded one group ahead)
-  const cu32x4* img = reinterpret_cast<const cu32x4*>(a.img);
-  cu32x4 wr[NLD];             // the next weight chunk (loaded one chunk ahead, across groups too)
-  auto gload = [&](int qq) {
-    qq = qq < a.nchunks ? qq : 0;   // past the last chunk: the next group's first
-    const int off = a.tab[2 * qq], sz = a.tab[2 * qq + 1];
-    const cu32x4* src = img + off;
+  const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, 0x7ffffff0, 0x00020000);
+  // weight chunks in flight two ahead, in two register sets: chunk c of a group sits in set c & 1 (the group's
+  // chunk count NCH is odd for KX = 1: the next group's chunks 0 / 1 are loaded into sets 0 / 1 by whichever
+  // of the last two chunks frees that set)
+  constexpr int NCH = KX + 14;
+  cu32x4 wr[2][NLD];
+  auto gload = [&](int set, int qq) {
+    if constexpr ((FUSED16_ABL & 4) != 0) return;
+    const int off = __builtin_amdgcn_readfirstlane(a.tab[2 * qq]);
+    const int sz = __builtin_amdgcn_readfirstlane(a.tab[2 * qq + 1]);
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int idx = threadIdx.x + i * NT;
-      wr[i] = src[idx < sz ? idx : sz - 1];
+      wr[set][i] = __builtin_bit_cast(
+          cu32x4, __builtin_amdgcn_raw_buffer_load_b128(rimg, (idx < sz ? idx : sz - 1) * 16, off * 16, 0));
     }
   };
-  gload(0);
+  gload(0, 0);
+  gload(1, 1);
 
   const int ngroups = fa.f.ngroups;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -239,10 +253,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int i = 0; i < NLD; ++i) {
         const int idx = threadIdx.x + i * NT;
-        if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[i];
+        if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[q & 1][i];
       }
-      lds_barrier();   // chunk q visible; every wave is past chunk q - 1, so buffer (q + 1) & 1 is free
-      gload(q + 1);
+      if constexpr ((FUSED16_ABL & 8) == 0) lds_barrier();   // chunk q visible; every wave is past chunk q - 1
+      gload(q & 1, q + 2 < NCH ? q + 2 : (q & 1));
       W = reinterpret_cast<const unsigned short*>(buf) + frag;
       ++q;
     };
@@ -285,6 +299,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     auto run = [&](auto& dacc, auto TI_, auto TJ_, int ti0, int e) __attribute__((always_inline)) {
       constexpr int TI = decltype(TI_)::value, TJ = decltype(TJ_)::value;
       constexpr int TWm = sizeof(dacc) / sizeof(f32x4);
+      if constexpr ((FUSED16_ABL & 2) != 0) return;
 #pragma unroll
       for (int k = 0; k < TWm; ++k) {
         const int u = wave + FW * k;
@@ -304,18 +319,25 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         }
       }
     };
-    // bias sums of layer m from acc-layout RD tiles: sum over the wave's 16 states
+    // bias sums of layer m from acc-layout RD tiles: the sum over the wave's 16 states (the lanes s of a row)
+    // of the lane's 4 features, transposed on the way so that the 4 values become 1: partner s^1 takes one
+    // pair, s^2 one value, then rotations by 4 and 8 within the row; lane s < 4 ends with feature
+    // 4g + 2(s & 1) + (s >> 1 & 1)
     auto bias_add = [&](int m, auto OT_, const f32x4 (&R)[OTM]) {
       constexpr int OT = decltype(OT_)::value;
+      const bool o1 = s & 1, o2 = (s >> 1) & 1;
 #pragma unroll
       for (int t = 0; t < OT; ++t) {
-        f32x4 v = R[t];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = sum16_dpp(v[j]);
-        if (s == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) sb[wave][m][16 * t + 4 * g + j] += v[j];
-        }
+        const f32x4 v = R[t];
+        float k0 = o1 ? v[2] : v[0], k1 = o1 ? v[3] : v[1];
+        const float t0 = o1 ? v[0] : v[2], t1 = o1 ? v[1] : v[3];
+        k0 += dpp_f<kDppX1>(t0);
+        k1 += dpp_f<kDppX1>(t1);
+        float k = o2 ? k1 : k0;
+        k += dpp_f<kDppX2>(o2 ? k0 : k1);
+        k += dpp_f<kDppRor4>(k);
+        k += dpp_f<kDppRor8>(k);
+        if (s < 4) sb[wave][m][16 * t + 4 * g + 2 * o1 + o2] += k;
       }
     };
     // this wave's max of a tensor whose per-state maxima are m -> sred[k][wave]; its group exponent
@@ -333,11 +355,13 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     auto rsrc = [&](const float* p, int ld) {
       return __builtin_amdgcn_make_buffer_rsrc((void*)(p + row_b * ld), 0, rb * ld * 4, 0x00020000);
     };
-    auto voff = [&](int ld, int t) {
+    auto voff = [&](int ld, int t) {   // columns past the width read zeros (offset past the buffer); branch-free
       const int col = 16 * t + 4 * g;
-      return col < ld ? (lrow * ld + col) * 4 : rb * ld * 4;
+      const int bad = -(int)(col >= ld);
+      return (((lrow * ld + col) * 4) & ~bad) | ((rb * ld * 4) & bad);
     };
     auto ld4 = [&](__amdgpu_buffer_rsrc_t r, int vo) -> f32x4 {
+      if constexpr ((FUSED16_ABL & 1) != 0) return f32x4{0.5f, 0.25f, 0.125f, 0.0625f};
       return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0));
     };
     auto bias4 = [&](int l, int t) -> f32x4 { return *reinterpret_cast<const f32x4*>(&sc[l][16 * t + 4 * g]); };
@@ -363,8 +387,9 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     };
 
     // One chain step: acc = [S (KC0 chunks, registers, times 2^eS per state) x job jS |
-    //                        M1 (KC1 chunks, memory, times sM) x job jS + 1], unscaled to f32 on return;
+    //                        M1 (KC1 chunks, memory, times sM) x job jS + 1]; acc * su is the f32 value;
     // the epilogue operand Pre is prefetched into PF; cap (optional) receives M1's split planes.
+    float su = 1.0f;
     auto step = [&](auto OT_, auto KC0_, auto KC1_, int jS, int eS, const float* M1, int ld1, float sM, int eM,
                     const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre) __attribute__((always_inline)) {
       constexpr int OT = decltype(OT_)::value, KC0 = decltype(KC0_)::value, KC1 = decltype(KC1_)::value;
@@ -427,9 +452,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         if (cap) putb(cap, c, b);
         mma(OT_, b);
       }
-      const int eu = -(ej[jM] + eM);
-#pragma unroll
-      for (int t = 0; t < OT; ++t) acc[t] = ldexp4(acc[t], eu);
+      su = __builtin_ldexpf(1.0f, -(ej[jM] + eM));
     };
 
     using C1 = std::integral_constant<int, 1>;
@@ -451,7 +474,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     for (int t = 0; t < OTM; ++t) {
       const f32x4 cb = bias4(0, t), h = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) RH1[t][i] = c_one_minus_sq(h[i]) * (acc[t][i] + cb[i]);
+      for (int i = 0; i < 4; ++i) RH1[t][i] = c_one_minus_sq(h[i]) * __builtin_fmaf(acc[t][i], su, cb[i]);
     }
     float mst = state_max<OTM>(RH1);
     wave_max(0, mst);
@@ -463,7 +486,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     for (int t = 0; t < OTM; ++t) {
       const f32x4 cb = bias4(1, t), h = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) RH2[t][i] = c_one_minus_sq(h[i]) * (acc[t][i] + cb[i]);
+      for (int i = 0; i < 4; ++i) RH2[t][i] = c_one_minus_sq(h[i]) * __builtin_fmaf(acc[t][i], su, cb[i]);
       H2f[t] = h;
     }
     mst = state_max<OTM>(RH2);
@@ -475,8 +498,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int t = 0; t < OTM; ++t) S[t] = RH2[t];
       step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false);
-      // f64 as chain.hip / fused.hip, bit for bit on the same z and p
-      float zf[8], pf[8];
+      // R-softmax in f32 on the cancellation-free form of tail.hip / gemm.hip kRHead:
+      //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k],
+      //   Rp = p (Rz - <p, Rz>), A = p / (p + eps), B = eps / (p + eps); the 4 lanes of a state hold 8 actions each
+      float zf[8], pf[8], inv[8];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const f32x4 cb = bias4(2, t);
@@ -484,28 +509,26 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool real = 16 * t + 4 * g + i < A;
-          zf[4 * t + i] = real ? acc[t][i] + cb[i] : 0.0f;
+          zf[4 * t + i] = real ? __builtin_fmaf(acc[t][i], su, cb[i]) : 0.0f;
           pf[4 * t + i] = real ? pv[i] : 0.0f;
         }
       }
-      double prz = 0.0;
+      float prz = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) prz += (double)pf[k] * (double)zf[k];
-      prz = sum4lanes(prz);
-      double spB = 0.0, sRAB = 0.0;
+      for (int k = 0; k < 8; ++k) prz = __builtin_fmaf(pf[k], zf[k], prz);
+      prz = xadd_f<true>(xadd_f<false>(prz));
+      float spB = 0.0f, sRAB = 0.0f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const bool real = 16 * (k >> 2) + 4 * g + (k & 3) < A;
-        const double pd = (double)pf[k];
-        const double Rp = pd * ((double)zf[k] - prz);
-        const double den = pd + (double)kEps;
-        const double Aa = real ? pd / den : 0.0;
-        const double B = real ? (double)kEps / den : 0.0;
-        spB += pd * B;
+        inv[k] = 1.0f / (pf[k] + kEps);
+        const float Rp = pf[k] * (zf[k] - prz);
+        const float Aa = pf[k] * inv[k], B = kEps * inv[k];
+        spB += pf[k] * B;
         sRAB += Rp * Aa * B;
       }
-      spB = sum4lanes(spB);
-      sRAB = sum4lanes(sRAB);
+      spB = xadd_f<true>(xadd_f<false>(spB));
+      sRAB = xadd_f<true>(xadd_f<false>(sRAB));
+      const float invN = (float)a.invN;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f32x4 r;
@@ -513,13 +536,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         for (int i = 0; i < 4; ++i) {
           const int k = 4 * t + i;
           const bool real = 16 * t + 4 * g + i < A;
-          const double pd = (double)pf[k];
-          const double Rp = pd * ((double)zf[k] - prz);
-          const double den = pd + (double)kEps;
-          const double Aa = real ? pd / den : 0.0;
-          const double B = real ? (double)kEps / den : 0.0;
-          const double rd = a.invN * (Rp * (B - spB) + Rp * Aa * Aa + pd * sRAB);
-          r[i] = real ? (float)rd : 0.0f;
+          const float Rp = pf[k] * (zf[k] - prz);
+          const float Aa = pf[k] * inv[k], B = kEps * inv[k];
+          const float rd = invN * (Rp * (B - spB) + Rp * Aa * Aa + pf[k] * sRAB);
+          r[i] = real ? rd : 0.0f;
         }
         S[t] = r;
       }
@@ -544,7 +564,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     for (int t = 0; t < OTM; ++t) {
       const f32x4 h = H2f[t], e = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH2[t][i], acc[t][i] * c_one_minus_sq(h[i]));
+      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH2[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
     }
     mst = state_max<OTM>(S);
     wave_max(3, mst);
@@ -579,7 +599,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     for (int t = 0; t < OTM; ++t) {
       const f32x4 h = H1f[t], e = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH1[t][i], acc[t][i] * c_one_minus_sq(h[i]));
+      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH1[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
     }
     mst = state_max<OTM>(S);
     wave_max(4, mst);
@@ -692,6 +712,7 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
   int maxb = 1;
   for (int i = 0; i < a.n; ++i) {
     const ChainImgJob& j = a.job[i];
+    if (j.K * j.O > kImgMax || j.K * j.O < 1) throw std::runtime_error("fused16 images: matrix size");
     if (j.which == which) maxb = std::max(maxb, (j.kc * j.otp * 4 + 255) / 256);
   }
   hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
@@ -700,7 +721,7 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
 void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) {
   if (grid <= 0) return;
   if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16 fvp: unsupported shape");
-  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16 fvp: chunk table");
+  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16 fvp: chunk table");  // NCH
   const int rb = fused16_states_per_group();
   if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16 fvp: group count does not match");
   switch (ti0_of(a.f.c.w[0])) {

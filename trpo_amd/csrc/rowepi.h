@@ -17,6 +17,9 @@
 #ifndef TRPO_EPI_TRACK
 #define TRPO_EPI_TRACK 1   // ablation builds only (tools): 0 drops the f16 running-max tracking
 #endif
+#ifndef TRPO_PREP_HEAD64
+#define TRPO_PREP_HEAD64 0 // 1: the prepare head's KL / surr logit deltas in f64 (round-4 form; A/B only)
+#endif
 #ifndef TRPO_HEAD_LOG64
 #define TRPO_HEAD_LOG64 0  // 1: the loss heads' logs in f64 (round-1 form; A/B only)
 #endif
@@ -73,6 +76,8 @@ __device__ __forceinline__ float hmax32(float v) {
   return v;
 }
 #endif
+__device__ __forceinline__ float hsum32t(float v) { return hsum32(v); }
+__device__ __forceinline__ double hsum32t(double v) { return hsum32d(v); }
 
 // workgroup max of v[i] >= 0 for the non-NULL slots, one atomicMax per slot per workgroup (float bits
 // order as unsigned for v >= 0) into the slot's counter for this block (kernels.h, kAmaxSub).
@@ -267,26 +272,33 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
       e.rowterms[4 * (size_t)row + 3] = 0.0;
     }
     if constexpr (EPI == (int)RowEpi::kPrepHead) {
-      // KL_ff plain logit delta (:56-57), cancellation-free:
+      // KL_ff plain logit delta (:56-57), cancellation-free, in f32 (f64 took 40 % of this launch at C4; the
+      // O(eps) terms it feeds reach Hv only through D and E, far below f32 rounding of Hv):
       //   d_j = (p_j/N) (B_j - sum_k p_k B_k),  B = eps/(p+eps)
-      double B[TN], spBp = 0.0, restp = 0.0;
+#if TRPO_PREP_HEAD64
+      typedef double T;
+#else
+      typedef float T;
+#endif
+      const T invN = (T)e.invN;
+      T B[TN], spBp = 0, restp = 0;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        const double pd = p[t];
-        B[t] = real[t] ? (double)kEps / (pd + (double)kEps) : 0.0;
+        const T pd = p[t];
+        B[t] = real[t] ? (T)kEps / (pd + (T)kEps) : T(0);
         spBp += pd * B[t];
-        restp += (real[t] && 32 * t + lr != a) ? pd : 0.0;
+        restp += (real[t] && 32 * t + lr != a) ? pd : T(0);
       }
-      const double spB = hsum32d(spBp);
-      const double rest = hsum32d(restp);   // 1 - p_a
+      const T spB = hsum32t(spBp);
+      const T rest = hsum32t(restp);   // 1 - p_a
       // surr logit delta (:54): -(adv/(N old_a)) p_a (1[j=a] - p_j)
-      const double coef = -(double)adv * e.invN / (double)olda * (double)pa;
+      const T coef = -(T)adv * invN / (T)olda * (T)pa;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         const int col = 32 * t + lr;
-        const double pd = p[t];
-        const double dl = real[t] ? pd * e.invN * (B[t] - spB) : 0.0;
-        const double ds = real[t] ? coef * (col == a ? rest : -pd) : 0.0;
+        const T pd = p[t];
+        const float dl = real[t] ? (float)(pd * invN * (B[t] - spB)) : 0.0f;
+        const float ds = real[t] ? (float)(coef * (col == a ? rest : -pd)) : 0.0f;
         if (st[t]) {
           const size_t sidx = (size_t)row * e.ldo + col;
           e.out0[sidx] = real[t] ? p[t] : 0.0f;
