@@ -39,6 +39,12 @@
 #ifndef FUSED16_ABL
 #define FUSED16_ABL 0
 #endif
+#ifndef FUSED16_RING
+#define FUSED16_RING 2   // memory-sourced B chunks loaded this many chunks ahead
+#endif
+#ifndef FUSED16_PFEARLY
+#define FUSED16_PFEARLY 1   // 1: a step's epilogue operand is loaded before its register segment, not its memory one
+#endif
 
 
 namespace trpo {
@@ -167,7 +173,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   constexpr int TW0 = (TI0 * OTM + FW - 1) / FW;   // owned gradient tiles: obs x hidden
   constexpr int TWH = (OTM * OTM + FW - 1) / FW;   //                       hidden x hidden
   constexpr int TWL = (OTM * OTA + FW - 1) / FW;   //                       hidden x actions
-  constexpr int RING = 2;
+  constexpr int RING = FUSED16_RING;
   __shared__ cu32x4 wl[2][CHU];
   __shared__ __attribute__((aligned(16))) unsigned short simg[2][2 * PL];   // [act | delta] images, hi / lo planes
   __shared__ float sb[FW][3][64];                                          // per-wave bias sums
@@ -397,20 +403,26 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int t = 0; t < OTM; ++t) acc[t] = z4;
       const __amdgpu_buffer_rsrc_t r1 = rsrc(M1, ld1);
-      const int oob1 = rb * ld1 * 4;
-      auto mld = [&](int cc, int h) { return ld4(r1, cc < KC1 ? voff(ld1, 2 * cc + h) : oob1); };
-      f32x4 n0 = z4, n1 = z4, m0 = z4, m1 = z4;
-      if (pre) {
-        n0 = xn0;
-        n1 = xn1;
-      } else if (KC0 < RING) {
-        n0 = mld(0, 0);
-        n1 = mld(0, 1);
-      }
-      if constexpr (KC0 == 0) {
-        m0 = mld(1, 0);
-        m1 = mld(1, 1);
-      }
+      // memory chunk j (step chunk KC0 + j) is loaded RING chunks ahead of its use, or at the step's start
+      f32x4 mb[KC1][2];
+      auto issue = [&](int j) {
+        if (j == 0 && pre) {   // X's first chunk, loaded during the previous group
+          mb[0][0] = xn0;
+          mb[0][1] = xn1;
+        } else {
+          mb[j][0] = ld4(r1, voff(ld1, 2 * j));
+          mb[j][1] = ld4(r1, voff(ld1, 2 * j + 1));
+        }
+      };
+      auto pf_load = [&]() {
+        const __amdgpu_buffer_rsrc_t rp = rsrc(Pre, ldp);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) PF[t] = ld4(rp, t < OTp ? voff(ldp, t) : rb * ldp * 4);
+      };
+      if constexpr (FUSED16_PFEARLY) pf_load();
+#pragma unroll
+      for (int j = 0; j < KC1; ++j)
+        if (KC0 + j < RING) issue(j);
       if constexpr (KC0 > 0) {
         const float sS = __builtin_amdgcn_ldexpf(1.0f, eS);
 #pragma unroll
@@ -418,14 +430,9 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
           fh8 b[2];
           mkb16(S[2 * c], S[2 * c + 1], sS, b);
           chunk_begin();
-          if (c == KC0 - RING) {
-            n0 = mld(0, 0);
-            n1 = mld(0, 1);
-          }
-          if (c == KC0 - 1) {
-            m0 = mld(1, 0);
-            m1 = mld(1, 1);
-          }
+#pragma unroll
+          for (int j = 0; j < KC1; ++j)
+            if (KC0 + j >= RING && KC0 + j - RING == c) issue(j);
           mma(OT_, b);
         }
         // segment scales: 2^(ej[jS] + eS) -> 2^(ej[jS + 1] + eM)
@@ -436,19 +443,11 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       const int jM = KC0 > 0 ? jS + 1 : jS;
 #pragma unroll
       for (int c = 0; c < KC1; ++c) {
-        const f32x4 x0 = n0, x1 = n1;
-        n0 = m0;
-        n1 = m1;
         chunk_begin();
-        m0 = mld(c + RING, 0);
-        m1 = mld(c + RING, 1);
-        if (c == 0) {
-          const __amdgpu_buffer_rsrc_t rp = rsrc(Pre, ldp);
-#pragma unroll
-          for (int t = 0; t < OTM; ++t) PF[t] = ld4(rp, t < OTp ? voff(ldp, t) : rb * ldp * 4);
-        }
+        if (c + RING < KC1 && KC0 + c + RING >= RING) issue(c + RING);
+        if (!FUSED16_PFEARLY && c == 0) pf_load();
         fh8 b[2];
-        mkb16(x0, x1, sM, b);
+        mkb16(mb[c][0], mb[c][1], sM, b);
         if (cap) putb(cap, c, b);
         mma(OT_, b);
       }
