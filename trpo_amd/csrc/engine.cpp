@@ -1435,8 +1435,12 @@ struct trpo_engine {
     fa.am_x = am_x();
     fa.am_d1 = am_d(1);
     fa.am_d2 = am_d(2);
-    const int grid = (int)std::max<int64_t>(
+    // persistent workgroups, at most one per slab: as few as take the same number of group rounds (fewer slabs
+    // for reduce_slab to sum)
+    const int64_t slots = std::max<int64_t>(
         1, std::min<int64_t>({(int64_t)fa.f.ngroups, (int64_t)S, (int64_t)num_cus * fused16_groups_per_cu()}));
+    const int64_t rounds = (fa.f.ngroups + slots - 1) / slots;
+    const int grid = (int)std::max<int64_t>(1, (fa.f.ngroups + rounds - 1) / rounds);
     {
       Scope sp(this, "fvp_fused");
       launch_fvp_fused16(fa, grid, stream);

@@ -119,6 +119,20 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
   const ChainImgJob& j = a.job[blockIdx.y];
   if (j.which != which) return;
   const float* src = (which ? v : theta) + j.src_off;
+  // this thread's 8 image values, loaded with the max's loads (one round trip to memory, not two)
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const bool live = idx < j.kc * j.otp * 4;
+  const int gg = idx & 3;
+  const int o = (idx >> 2) % j.otp;
+  const int c = (idx >> 2) / j.otp;
+  float x[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = 32 * c + chain_perm(8 * gg + q);
+    const bool in = live && o < j.O && k < j.K;
+    const float val = src[in ? (j.trans ? o * j.ldw + k : k * j.ldw + o) : 0];
+    x[q] = in ? val : 0.0f;
+  }
   float m = 0.0f;
   const int last = j.K * j.O - 1;   // W_l is K x O or O x K, dense, at most 128 x 64: 32 loads in flight per lane
 #pragma unroll
@@ -130,19 +144,10 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const int e = f16_scale_exp(m);
   if (blockIdx.x == 0 && threadIdx.x == 0) img_e[blockIdx.y] = e;
+  if (!live) return;
   const float sc = __builtin_ldexpf(1.0f, e);
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= j.kc * j.otp * 4) return;
-  const int gg = idx & 3;
-  const int o = (idx >> 2) % j.otp;
-  const int c = (idx >> 2) / j.otp;
-  float x[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int k = 32 * c + chain_perm(8 * gg + q);
-    x[q] = 0.0f;
-    if (o < j.O && k < j.K) x[q] = (j.trans ? src[(size_t)o * j.ldw + k] : src[(size_t)k * j.ldw + o]) * sc;
-  }
+  for (int q = 0; q < 8; ++q) x[q] *= sc;
   cu32x4 H, L;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
