@@ -472,7 +472,7 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
       const int av = a.act[row];
       const float adv = a.adv[row];
       float pa = 0.0f, olda = 0.0f;
-      double klp = 0.0, enp = 0.0;
+      float klp = 0.0f, enp = 0.0f;
 #pragma unroll
       for (int j = 0; j < AT; ++j) {
         if (j < a.A) {
@@ -481,9 +481,10 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
             pa = p[j];
             olda = oj;
           }
-          // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs, f64 row sums
-          klp += (double)oj * (double)logf((oj + kEps) / (p[j] + kEps));
-          enp += -(double)p[j] * (double)logf(p[j] + kEps);
+          // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs and row sums (gemm.hip's
+          // row heads alike); the sums over rows are f64
+          klp += oj * logf((oj + kEps) / (p[j] + kEps));
+          enp += -p[j] * logf(p[j] + kEps);
         }
       }
       double* rt = a.rowterms + 4 * row;
@@ -493,17 +494,17 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
       rt[3] = 0.0;
       if constexpr (PREP) {
         // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps); surr logit delta
-        // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead)
-        // (B_j is recomputed in the output loop instead of held: a double array of AT entries costs 2 AT VGPRs)
-        double spB = 0.0, rest = 0.0;
+        // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead), in f32 as there
+        // (B_j is recomputed in the output loop instead of held: AT more VGPRs)
+        const float invN = (float)a.invN;
+        float spB = 0.0f, rest = 0.0f;
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
-          const double pd = p[j];
-          const double Bj = j < a.A ? (double)kEps / (pd + (double)kEps) : 0.0;
-          spB += pd * Bj;
-          rest += (j < a.A && j != av) ? pd : 0.0;
+          const float Bj = j < a.A ? kEps / (p[j] + kEps) : 0.0f;
+          spB += p[j] * Bj;
+          rest += (j < a.A && j != av) ? p[j] : 0.0f;
         }
-        const double coef = -(double)adv * a.invN / (double)olda * (double)pa;
+        const float coef = -adv * invN / olda * pa;
         float* Pr = a.P + row * a.Apad;
         float* Dr = a.D + row * a.Apad;
         float* Sr = a.DS + row * a.Apad;
@@ -511,11 +512,11 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
         for (int j = 0; j < AT; ++j) {
           if (j < a.Apad) {
             const bool real = j < a.A;
-            double pd = p[j];
-            asm volatile("" : "+v"(pd));   // recomputed, not kept from the first loop (CSE would hold AT doubles)
-            const double Bj = real ? (double)kEps / (pd + (double)kEps) : 0.0;
-            const float dl = real ? (float)(pd * a.invN * (Bj - spB)) : 0.0f;
-            const float ds = real ? (float)(coef * (j == av ? rest : -pd)) : 0.0f;
+            float pd = p[j];
+            asm volatile("" : "+v"(pd));   // recomputed, not kept from the first loop
+            const float Bj = real ? kEps / (pd + kEps) : 0.0f;
+            const float dl = real ? pd * invN * (Bj - spB) : 0.0f;
+            const float ds = real ? coef * (j == av ? rest : -pd) : 0.0f;
             Pr[j] = real ? p[j] : 0.0f;
             Dr[j] = dl;
             Sr[j] = ds;

@@ -247,23 +247,30 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
     const float pa = __shfl(pa_l, a & 31, 32);
     const float olda = __shfl(olda_l, a & 31, 32);
     const float adv = rowvalid ? advv : 0.0f;
-    // row loss terms (:46-51), accumulated in f64
+    // row loss terms (:46-51)
+#if TRPO_HEAD_LOG64
     double klp = 0.0, enp = 0.0;
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
-#if TRPO_HEAD_LOG64
       const double pd = p[t], od = old[t];
       klp += real[t] ? od * log((od + (double)kEps) / (pd + (double)kEps)) : 0.0;
       enp += real[t] ? -pd * log(pd + (double)kEps) : 0.0;
-#else
-      // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs, f64 row sums
-      const float lk = logf((old[t] + kEps) / (p[t] + kEps)), le = logf(p[t] + kEps);
-      klp += real[t] ? (double)old[t] * (double)lk : 0.0;
-      enp += real[t] ? -(double)p[t] * (double)le : 0.0;
-#endif
     }
     const double klt = hsum32d(klp);
     const double ent = hsum32d(enp);
+#else
+    // the reference's own precision (f32 tensors, trpo_inksci.py:50-51): f32 logs and f32 row sums of <= 32 TN
+    // terms; the sums over rows are f64 (rowterms)
+    float klp = 0.0f, enp = 0.0f;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const float lk = logf((old[t] + kEps) / (p[t] + kEps)), le = logf(p[t] + kEps);
+      klp += real[t] ? old[t] * lk : 0.0f;
+      enp += real[t] ? -p[t] * le : 0.0f;
+    }
+    const double klt = hsum32(klp);
+    const double ent = hsum32(enp);
+#endif
     const double sur = rowvalid ? (double)pa / (double)olda * (double)adv : 0.0;
     if (rowvalid && lr == 0) {
       e.rowterms[4 * (size_t)row + 0] = sur;
