@@ -6,7 +6,8 @@
 #   bash tools/gpu.sh smoke <name>                      __graft_entry__.smoke()
 #   bash tools/gpu.sh bench <name> <config>... [-- bench args]   one bench line per config (+ HIP-event profile)
 #   bash tools/gpu.sh ab <name> <config> <rounds> "<env A>" "<env B>" ...   interleaved same-box A/B of env
-#                                                        settings ("" = defaults; TRPO_ENGINE_LIB=... picks a build)
+#                                                        settings ("" = defaults; TRPO_ENGINE_LIB=... picks a build;
+#                                                        AB_STEPS / AB_ARGS: steps and extra bench arguments)
 #   bash tools/gpu.sh prof <name> [bench args]          rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes
 #   bash tools/gpu.sh sq <name> [bench args]            SQ / GRBM counter passes per kernel (pmc_kernels.sh)
 #   bash tools/gpu.sh round <name>                      tests + smoke + C4 (with CPU baseline) / C3 / C2 / C5 lines
@@ -54,7 +55,7 @@ case $CMD in
       i=0
       for e in "$@"; do
         timeout -k 10 300 env $e python -u bench.py --config $CFG --steps ${AB_STEPS:-5} --warmup 2 --no-cpu-baseline \
-          --no-alt --profile-out $OUT/ab_${i}_$r.prof.json > $OUT/ab_${i}_$r.json 2> $OUT/ab_${i}_$r.err \
+          --no-alt ${AB_ARGS:-} --profile-out $OUT/ab_${i}_$r.prof.json > $OUT/ab_${i}_$r.json 2> $OUT/ab_${i}_$r.err \
           || { echo "variant [$e] failed"; tail -5 $OUT/ab_${i}_$r.err; exit 1; }
         summ $OUT/ab_${i}_$r.json "[$e] round $r" | tee -a $OUT/ab.txt
         i=$((i+1))

@@ -390,6 +390,10 @@ struct trpo_engine {
     const int64_t slab_bytes = (int64_t)slab_stride * 4;
     auto fit = [&](int64_t bytes) { return std::max<int64_t>(1, bytes / slab_bytes); };
     s_target = (int)std::max<int64_t>(s_target, std::min<int64_t>(fit(int64_t(2) << 30), (cap + 16383) / 16384));
+    // wide single-tile layers (C4) with few rows (a rank of a 2-8 GPU run): one split per CU when the rows allow it,
+    // i.e. one round of the one-workgroup-per-CU split kernels and half the slab reduction (1M rows: 58.3 -> 57.2
+    // ms per update, 2M: 111.1 -> 110.4; 128 splits lose half the CUs, profiles/r5u)
+    if (tiles_max == 1 && s_target == 512 && num_cus < 512 && (cap + 16383) / 16384 <= num_cus) s_target = num_cus;
     if (g_options.splits > 0) s_target = std::min(g_options.splits, 8192);
     int s_pg = (int)std::max<int64_t>(
         s_target, std::min<int64_t>({2048, std::max<int64_t>(4 * (int64_t)s_target, (cap + 4095) / 4096),
