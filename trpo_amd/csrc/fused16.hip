@@ -42,6 +42,9 @@
 #ifndef FUSED16_RING
 #define FUSED16_RING 2   // memory-sourced B chunks loaded this many chunks ahead
 #endif
+#ifndef FUSED16_WSETS
+#define FUSED16_WSETS 2   // weight chunks in flight (register sets)
+#endif
 #ifndef FUSED16_PFEARLY
 #define FUSED16_PFEARLY 1   // 1: a step's epilogue operand is loaded before its register segment, not its memory one
 #endif
@@ -224,11 +227,12 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   f32x4 H2f[OTM], H1f[OTM];
   f32x4 xn0 = z4, xn1 = z4;   // first X chunk of the next group (loaded one group ahead)
   const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, 0x7ffffff0, 0x00020000);
-  // weight chunks in flight two ahead, in two register sets: chunk c of a group sits in set c & 1 (the group's
-  // chunk count NCH is odd for KX = 1: the next group's chunks 0 / 1 are loaded into sets 0 / 1 by whichever
-  // of the last two chunks frees that set)
+  // weight chunks in flight WS ahead, in WS register sets: chunk c of a group sits in set c % WS (the group's
+  // chunk count NCH need not be a multiple of WS: the next group's chunk k < WS is loaded into set k by whichever
+  // of the last WS chunks frees that set)
   constexpr int NCH = KX + 14;
-  cu32x4 wr[2][NLD];
+  constexpr int WS = FUSED16_WSETS;
+  cu32x4 wr[WS][NLD];
   auto gload = [&](int set, int qq) {
     if constexpr ((FUSED16_ABL & 4) != 0) return;
     const int off = __builtin_amdgcn_readfirstlane(a.tab[2 * qq]);
@@ -240,8 +244,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
           cu32x4, __builtin_amdgcn_raw_buffer_load_b128(rimg, (idx < sz ? idx : sz - 1) * 16, off * 16, 0));
     }
   };
-  gload(0, 0);
-  gload(1, 1);
+#pragma unroll
+  for (int k = 0; k < WS; ++k) gload(k, k);
 
   const int ngroups = fa.f.ngroups;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -264,10 +268,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int i = 0; i < NLD; ++i) {
         const int idx = threadIdx.x + i * NT;
-        if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[q & 1][i];
+        if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[q % WS][i];
       }
       if constexpr ((FUSED16_ABL & 8) == 0) lds_barrier();   // chunk q visible; every wave is past chunk q - 1
-      gload(q & 1, q + 2 < NCH ? q + 2 : (q & 1));
+      gload(q % WS, q + WS < NCH ? q + WS : q % WS);
       W = reinterpret_cast<const unsigned short*>(buf) + frag;
       ++q;
     };
