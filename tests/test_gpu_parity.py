@@ -340,6 +340,38 @@ def test_kernel_variants_parity(gpu_available, opts):
 
 
 @pytest.mark.parametrize("obs,hidden,A,n", [
+    (11, [64, 64], 3, 3001),           # C2 dims, partial last group
+    (128, [64, 64], 18, 100_000),      # C3 dims, many groups per persistent workgroup
+    (40, [64, 49], 32, 777),           # 4 obs tiles, a partial hidden tile, A = 32
+    (20, [56, 64], 17, 1),             # one state
+])
+def test_fused16_policy_grad_vs_oracle(gpu_available, obs, hidden, A, n):
+    """The policy gradient in one launch (fused16.hip's PG form, fused = 3) against the float64 oracle and the
+    row-GEMM backward + weight-gradient path (fused = 2), deterministic (trpo_inksci.py:54, utils.py:160)."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + 11)
+    ref = O.policy_grad(dd["theta"].astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    saved = get_option("fused")
+    out = {}
+    try:
+        for mode in (3, 2):
+            set_option("fused", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            out[mode] = e.policy_grad()
+            out[(mode, "again")] = e.policy_grad()
+            e.close()
+    finally:
+        set_option("fused", saved)
+    assert_vec_close(out[3], ref, REL, f"fused16 g {obs} {hidden} {A} n={n}")
+    assert_vec_close(out[3], out[2], REL, f"fused16 vs row-GEMM g {obs} {hidden} {A} n={n}")
+    assert np.array_equal(out[3], out[(3, "again")]), "fused16 policy gradient is not deterministic"
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
     (37, [200, 72, 144], 5, 1337),     # odd widths, 3 hidden layers, 16 register tiles, partial workgroup
     (128, [256, 256], 18, 3001),       # C4 dims, two head tiles
     (11, [64], 32, 500),               # one hidden layer (the reference policy's depth), A = 32

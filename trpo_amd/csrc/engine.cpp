@@ -1068,10 +1068,10 @@ struct trpo_engine {
   }
 
   // sum over splits -> out (local partial) ; all-reduce
-  void reduce_grad(float* out, const int* skip) {
+  void reduce_grad(float* out, const int* skip, int slabs = 0) {
     {
       Scope sp(this, "reduce");
-      launch_reduce_slab(slab, active_splits, slab_stride, P, out, skip, stream);
+      launch_reduce_slab(slab, slabs > 0 ? slabs : active_splits, slab_stride, P, out, skip, stream);
       check_launch();
     }
     allreduce_f32(out, (size_t)P);
@@ -1108,6 +1108,10 @@ struct trpo_engine {
   // flatgrad(surr) (trpo_inksci.py:54) -> g (all ranks)
   void policy_grad() {
     prepare();
+    if (use_fused16()) {
+      pg_fused16();
+      return;
+    }
     ensure_w3();
     PgSplits pgs(this);
     // surr backward: DS_{l-1} = (DS_l W_l^T)(1-H_l^2) ; DS of hidden layers lives in RD scratch
@@ -1412,19 +1416,9 @@ struct trpo_engine {
     allreduce_f32(out, (size_t)P);
   }
 
-  // the whole Hv in one launch on the f16 split (fused16.hip) + the slab reduction
-  void fvp_fused16(const float* v, float* out, const int* skip) {
-    if (!f16_w_valid) {
-      Scope sp(this, "fvp_img_w");
-      launch_fused16_img(f16_jobs, theta, v, 0, nullptr, f16_e, stream);
-      check_launch();
-      f16_w_valid = true;
-    }
-    {
-      Scope sp(this, "fvp_img_v");
-      launch_fused16_img(f16_jobs, theta, v, 1, skip, f16_e, stream);
-      check_launch();
-    }
+  // fused16.hip's arguments for the tangent v (the FVP) or none (the policy gradient), and its grid: persistent
+  // workgroups, at most one per slab, as few as take the same number of group rounds (fewer slabs to reduce)
+  Fused16Args fused16_args(const float* v, const int* skip, int& grid) {
     const int rb = fused16_states_per_group();
     Fused16Args fa{};
     fa.f.c = chain_args(v, skip);
@@ -1439,12 +1433,32 @@ struct trpo_engine {
     fa.am_x = am_x();
     fa.am_d1 = am_d(1);
     fa.am_d2 = am_d(2);
-    // persistent workgroups, at most one per slab: as few as take the same number of group rounds (fewer slabs
-    // for reduce_slab to sum)
+    fa.DS = DSL;
+    fa.am_ds2 = am_ds(L - 1);
     const int64_t slots = std::max<int64_t>(
         1, std::min<int64_t>({(int64_t)fa.f.ngroups, (int64_t)S, (int64_t)num_cus * fused16_groups_per_cu()}));
     const int64_t rounds = (fa.f.ngroups + slots - 1) / slots;
-    const int grid = (int)std::max<int64_t>(1, (fa.f.ngroups + rounds - 1) / rounds);
+    grid = (int)std::max<int64_t>(1, (fa.f.ngroups + rounds - 1) / rounds);
+    return fa;
+  }
+  void fused16_w_images() {
+    if (f16_w_valid) return;
+    Scope sp(this, "fvp_img_w");
+    launch_fused16_img(f16_jobs, theta, nullptr, 0, nullptr, f16_e, stream);
+    check_launch();
+    f16_w_valid = true;
+  }
+
+  // the whole Hv in one launch on the f16 split (fused16.hip) + the slab reduction
+  void fvp_fused16(const float* v, float* out, const int* skip) {
+    fused16_w_images();
+    {
+      Scope sp(this, "fvp_img_v");
+      launch_fused16_img(f16_jobs, theta, v, 1, skip, f16_e, stream);
+      check_launch();
+    }
+    int grid = 1;
+    const Fused16Args fa = fused16_args(v, skip, grid);
     {
       Scope sp(this, "fvp_fused");
       launch_fvp_fused16(fa, grid, stream);
@@ -1456,6 +1470,20 @@ struct trpo_engine {
       check_launch();
     }
     allreduce_f32(out, (size_t)P);
+  }
+
+  // g in one launch on the same machinery (fused16.hip, PG form): the surr backward from DS_2 and every block of g
+  void pg_fused16() {
+    fused16_w_images();
+    int grid = 1;
+    const Fused16Args fa = fused16_args(nullptr, nullptr, grid);
+    {
+      Scope sp(this, "pg_fused");
+      launch_pg_fused16(fa, grid, stream);
+      check_launch();
+    }
+    ds_ready = false;
+    reduce_grad(g, nullptr, grid);
   }
 
   // the same Hv with the row-local part (R-forward, R-head, R-backward) in one fused launch

@@ -166,8 +166,9 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
 // image jobs (kernels.h, kFused16Jobs)
 enum { jV0 = 0, jW1, jV1, jW2, jV2, jW2t, jV2t, jW1t, jV1t };
 
-// FW = waves per workgroup, TI0 = 16-feature tiles of obs (1, 2, 4, 8), OTA = 16-action tiles of the head
-template <int FW, int LB, int TI0, int OTA>
+// FW = waves per workgroup, TI0 = 16-feature tiles of obs (1, 2, 4, 8), OTA = 16-action tiles of the head;
+// PG: the policy gradient instead of the FVP (the same machinery on the backward chain alone)
+template <int FW, int LB, int TI0, int OTA, bool PG>
 __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16Args fa) {
   constexpr int OTM = 4;                       // 16-feature tiles of a hidden layer
   constexpr int NT = FW * 64;
@@ -197,15 +198,16 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   unsigned short* const sD = &simg[1][0];
 
   for (int i = threadIdx.x; i < FW * 3 * 64; i += NT) (&sb[0][0][0])[i] = 0.0f;
-  for (int i = threadIdx.x; i < 3 * 64; i += NT) {
+  for (int i = threadIdx.x; i < 3 * 64; i += NT) {   // (no tangent in the policy gradient)
     const int l = i >> 6, j = i & 63;
-    sc[l][j] = j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
+    sc[l][j] = !PG && j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
   }
 
   // scale exponents (wave-uniform)
   const int eX = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_x));
   const int eD1 = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_d1));
   const int eD2 = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_d2));
+  const int eDS = PG ? __builtin_amdgcn_readfirstlane(amax_exp(fa.am_ds2)) : 0;
   const int eH = f16_scale_exp(1.0f);
   int ej[kFused16Jobs];
 #pragma unroll
@@ -230,7 +232,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // weight chunks in flight WS ahead, in WS register sets: chunk c of a group sits in set c % WS (the group's
   // chunk count NCH need not be a multiple of WS: the next group's chunk k < WS is loaded into set k by whichever
   // of the last WS chunks frees that set)
-  constexpr int NCH = KX + 14;
+  constexpr int NCH = PG ? 3 : KX + 14;   // chunks per group
+  // image chunk (table index) of the group's chunk q: the FVP streams the whole image, the policy gradient
+  // W_2^T (one chunk) and W_1^T (two)
+  auto chunk_of = [&](int q) { return PG ? (q == 0 ? KX + 8 : KX + 9 + q) : q; };
   constexpr int WS = FUSED16_WSETS;
   cu32x4 wr[WS][NLD];
   auto gload = [&](int set, int qq) {
@@ -245,7 +250,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
   };
 #pragma unroll
-  for (int k = 0; k < WS; ++k) gload(k, k);
+  for (int k = 0; k < WS; ++k) gload(k, chunk_of(k));
 
   const int ngroups = fa.f.ngroups;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -271,7 +276,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         if (CHU % NT == 0 || idx < CHU) buf[idx] = wr[q % WS][i];
       }
       if constexpr ((FUSED16_ABL & 8) == 0) lds_barrier();   // chunk q visible; every wave is past chunk q - 1
-      gload(q % WS, q + WS < NCH ? q + WS : q % WS);
+      gload(q % WS, chunk_of(q + WS < NCH ? q + WS : q % WS));
       W = reinterpret_cast<const unsigned short*>(buf) + frag;
       ++q;
     };
@@ -402,7 +407,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     };
 
     // One chain step: acc = [S (KC0 chunks, registers, times 2^eS per state) x job jS |
-    //                        M1 (KC1 chunks, memory, times sM) x job jS + 1]; acc * su is the f32 value;
+    //                        M1 (KC1 chunks, memory, times sM) x job jS + 1 (jS when KC0 = 0)];
+    // acc * su is the f32 value;
     // the epilogue operand Pre is prefetched into PF; cap (optional) receives M1's split planes.
     float su = 1.0f;
     auto step = [&](auto OT_, auto KC0_, auto KC1_, int jS, int eS, const float* M1, int ld1, float sM, int eM,
@@ -413,7 +419,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       for (int t = 0; t < OTM; ++t) acc[t] = z4;
       const __amdgpu_buffer_rsrc_t r1 = rsrc(M1, ld1);
       // memory chunk j (step chunk KC0 + j) is loaded RING chunks ahead of its use, or at the step's start
-      f32x4 mb[KC1][2];
+      f32x4 mb[KC1 > 0 ? KC1 : 1][2];
       auto issue = [&](int j) {
         if (j == 0 && pre) {   // X's first chunk, loaded during the previous group
           mb[0][0] = xn0;
@@ -444,10 +450,11 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
             if (KC0 + j >= RING && KC0 + j - RING == c) issue(j);
           mma(OT_, b);
         }
-        // segment scales: 2^(ej[jS] + eS) -> 2^(ej[jS + 1] + eM)
-        const int d = ej[jS + 1] + eM - ej[jS] - eS;
+        if constexpr (KC1 > 0) {   // segment scales: 2^(ej[jS] + eS) -> 2^(ej[jS + 1] + eM)
+          const int d = ej[jS + 1] + eM - ej[jS] - eS;
 #pragma unroll
-        for (int t = 0; t < OT; ++t) acc[t] = ldexp4(acc[t], d);
+          for (int t = 0; t < OT; ++t) acc[t] = ldexp4(acc[t], d);
+        }
       }
       const int jM = KC0 > 0 ? jS + 1 : jS;
 #pragma unroll
@@ -460,7 +467,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         if (cap) putb(cap, c, b);
         mma(OT_, b);
       }
-      su = __builtin_ldexpf(1.0f, -(ej[jM] + eM));
+      // (a register-only step leaves its per-state scale: su is then per lane)
+      su = KC1 > 0 ? __builtin_ldexpf(1.0f, -(ej[jM] + eM)) : __builtin_amdgcn_ldexpf(1.0f, -(ej[jS] + eS));
     };
 
     using C1 = std::integral_constant<int, 1>;
@@ -469,6 +477,90 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     using COTA = std::integral_constant<int, OTA>;
     using CKX = std::integral_constant<int, KX>;
     using C0 = std::integral_constant<int, 0>;
+
+    if constexpr (PG) {
+      // ---- policy gradient (trpo_inksci.py:54): DS_1 = (DS_2 W_2^T)(1 - H_2^2),
+      //      DS_0 = (DS_1 W_1^T)(1 - H_1^2); g_W_l = H_l^T DS_l (H_0 = X), g_b_l = colsum DS_l.
+      //      DS_2 is the head's surr logit delta from the prepare pass. ----
+      const float sDS = __builtin_ldexpf(1.0f, eDS);
+      step(C4{}, C0{}, C1{}, jW2t, 0, fa.DS, a.ld[3], sDS, eDS, a.H[2], a.ld[2], OTM, sD, false);
+      f32x4 DS1[OTM];
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) {
+        const f32x4 h = PF[t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) DS1[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));
+        put4(sA, t, h, sH);   // H_2, the head layer's pass operand (sA is free: past this step's chunk barrier)
+      }
+      float mst = state_max<OTM>(DS1);
+      wave_max(3, mst);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) S[t] = DS1[t];
+      step(C4{}, C2{}, C0{}, jW1t, f16_scale_exp(mst), a.H[1], 0, 1.0f, 0, a.H[1], a.ld[1], OTM, nullptr, false);
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) {
+        const f32x4 h = PF[t];
+        H1f[t] = h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));   // DS_0
+      }
+      wave_max(4, state_max<OTM>(S));
+      const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
+      f32x4 nxt[OTM];
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], t));
+      {
+        // g_W_2 += H_2^T DS_2 (both images written above); g_b_2 from DS_2's f32 tiles
+        f32x4 d2[OTM];
+        const __amdgpu_buffer_rsrc_t rd = rsrc(fa.DS, a.ld[3]);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) d2[t] = t < OTA ? ld4(rd, voff(a.ld[3], t)) : z4;
+        lds_barrier();
+        bias_add(2, COTA{}, d2);
+        run(dwl, C4{}, COTA{}, 0, eH + eDS);
+      }
+      {
+        // g_W_1 += H_1^T DS_1
+        lds_barrier();
+        const int eg = group_exp(3);
+        const float sg = __builtin_ldexpf(1.0f, eg);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) {
+          put4(sD, t, DS1[t], sg);
+          put4(sA, t, H1f[t], sH);
+        }
+        bias_add(1, C4{}, DS1);
+        lds_barrier();
+        run(dwh, C4{}, C4{}, 0, eH + eg);
+      }
+      {
+        // g_W_0 += X^T DS_0 in 64-feature chunks of X
+        lds_barrier();
+        const int eg = group_exp(4);
+        const float sg = __builtin_ldexpf(1.0f, eg);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) {
+          put4(sD, t, S[t], sg);
+          put4(sA, t, nxt[t], sX);
+        }
+        bias_add(0, C4{}, S);
+#pragma unroll
+        for (int ch = 0; ch < OBC; ++ch) {
+          if (ch + 1 < OBC) {
+#pragma unroll
+            for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], 4 * (ch + 1) + t));
+          }
+          lds_barrier();
+          run(dw0, std::integral_constant<int, TI0>{}, C4{}, 4 * ch, eX + eg);
+          if (ch + 1 < OBC) {
+            lds_barrier();
+#pragma unroll
+            for (int t = 0; t < OTM; ++t) put4(sA, t, nxt[t], sX);
+          }
+        }
+      }
+      continue;
+    }
 
     if (grp == (int)blockIdx.x) {   // later groups' first X chunk is loaded during the previous group
       const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
@@ -695,13 +787,29 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 
 int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
 
-template <int TI0>
+template <int TI0, bool PG>
 void launch_ti0(const Fused16Args& a, int grid, hipStream_t s) {
   constexpr int FW = FUSED16_FW, LB = FUSED16_LB;
   if (a.f.c.w[3] <= 16)
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1>), dim3(grid), dim3(FW * 64), 0, s, a);
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1, PG>), dim3(grid), dim3(FW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2>), dim3(grid), dim3(FW * 64), 0, s, a);
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2, PG>), dim3(grid), dim3(FW * 64), 0, s, a);
+}
+
+template <bool PG>
+void launch_fused16(const Fused16Args& a, int grid, hipStream_t s) {
+  if (grid <= 0) return;
+  if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16: unsupported shape");
+  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16: chunk table");
+  const int rb = fused16_states_per_group();
+  if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16: group count does not match");
+  if (PG && !a.DS) throw std::runtime_error("fused16 policy gradient: no head delta");
+  switch (ti0_of(a.f.c.w[0])) {
+    case 1: launch_ti0<1, PG>(a, grid, s); break;
+    case 2: launch_ti0<2, PG>(a, grid, s); break;
+    case 4: launch_ti0<4, PG>(a, grid, s); break;
+    default: launch_ti0<8, PG>(a, grid, s); break;
+  }
 }
 
 }  // namespace
@@ -726,18 +834,7 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
   hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
 }
 
-void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) {
-  if (grid <= 0) return;
-  if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16 fvp: unsupported shape");
-  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16 fvp: chunk table");  // NCH
-  const int rb = fused16_states_per_group();
-  if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16 fvp: group count does not match");
-  switch (ti0_of(a.f.c.w[0])) {
-    case 1: launch_ti0<1>(a, grid, s); break;
-    case 2: launch_ti0<2>(a, grid, s); break;
-    case 4: launch_ti0<4>(a, grid, s); break;
-    default: launch_ti0<8>(a, grid, s); break;
-  }
-}
+void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<false>(a, grid, s); }
+void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<true>(a, grid, s); }
 
 }  // namespace trpo

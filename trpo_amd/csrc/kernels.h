@@ -394,6 +394,8 @@ struct Fused16Args {
   const unsigned* am_x;              // running-max slots: X, D_1, D_2
   const unsigned* am_d1;
   const unsigned* am_d2;
+  const float* DS;                   // policy gradient only: the head's surr logit delta DS_2 [n][ld 3] and its slot
+  const unsigned* am_ds2;
 };
 bool fused16_eligible(int L, const int* w);
 int fused16_obs_chunks(int obs);     // 32-deep k-chunks of V_0's image (obs rounded to 32, 64 or 128)
@@ -402,6 +404,9 @@ int fused16_groups_per_cu();
 void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
                         int* img_e, hipStream_t s);
 void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s);
+// The policy gradient of the same shapes in one launch (fused16.hip, PG form): DS_1, DS_0 by the backward chain
+// over W_2^T / W_1^T's image chunks and g's blocks H_l^T DS_l + colsum DS_l into the slabs, as the FVP's.
+void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
