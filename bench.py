@@ -96,6 +96,10 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return n * chain_flops_per_row(widths)
     if tag == "fvp_fused":            # fused.hip: the whole FVP incl. weight R-gradients
         return n * fvp_flops_per_row(widths)
+    if tag == "pg_fused":             # fused16.hip PG form: the surr backward below the head + every H_l^T DS_l
+        w = widths
+        L = len(w) - 1
+        return 2.0 * n * (sum(w[l] * w[l + 1] for l in range(1, L)) + sum(w[l] * w[l + 1] for l in range(L)))
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0
@@ -120,7 +124,7 @@ def tag_flops(tag: str, widths, n: int) -> float:
 def tag_is_split(tag: str, widths) -> bool:
     """Whether the kernel behind a tag runs on the split-bf16 MFMA path (gemm.hip dispatch rules)."""
     from trpo_amd._lib import get_option
-    if tag in ("fvp_chain", "fvp_fused"):
+    if tag in ("fvp_chain", "fvp_fused", "pg_fused"):
         return True
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
@@ -151,7 +155,7 @@ def tag_products(tag: str, widths) -> int:
     split (6), fused16.hip the scaled f16 hi+lo (3), the row GEMMs the engine's split option."""
     if tag == "fvp_chain" or (tag == "fvp_fused" and not fused16_used(widths)):
         return 6
-    return 3 if tag == "fvp_fused" else split_products()
+    return 3 if tag in ("fvp_fused", "pg_fused") else split_products()
 
 
 def tag_peak(tag: str, widths) -> float:
@@ -167,6 +171,8 @@ def tag_bytes(tag: str, widths, n: int) -> float:
         L = len(widths) - 1
         cols = widths[0] + 2 * widths[L] + 2 * sum(widths[1:L]) + sum(widths[2:L])
         return 4.0 * n * cols
+    if tag == "pg_fused":             # X, DS_{L-1}, H_l
+        return 4.0 * n * sum(widths)
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0
@@ -219,7 +225,7 @@ def tail_used(widths) -> bool:
 def tag_x_bytes(tag: str, widths, n: int) -> float:
     """SURVEY.md §8(d)'s algorithmic bytes of one launch: the states' X rows (N*obs*4) when the kernel
     reads X, else 0 (every other operand is an intermediate the algorithm need not materialise)."""
-    if tag in ("fvp_chain", "fvp_fused"):
+    if tag in ("fvp_chain", "fvp_fused", "pg_fused"):
         return 4.0 * n * widths[0]
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():

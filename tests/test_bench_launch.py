@@ -142,3 +142,31 @@ def test_rank_digest_sees_every_bit():
     w.view(np.uint32)[3] ^= 1                      # one ulp of one element
     assert bench.rank_digest([w, v[1]], stats) != d0
     assert bench.rank_digest(v, dict(stats, rdotr=np.nextafter(1.0, 2.0))) != d0
+
+
+def test_fused_fvp_roofline_follows_the_issued_arithmetic():
+    """The one-launch FVP is priced at the peak of the split it issues: f16 hi+lo (3 products) for fused16.hip's
+    shapes with fused = 3, the exact bf16 split (6) for fused.hip; the fused policy gradient at 3, with its FLOPs
+    (backward below the head + every weight gradient) and bytes (X, H_l, DS_{L-1})."""
+    from trpo_amd._lib import get_option, set_option
+    c3 = [128, 64, 64, 18]
+    saved = get_option("fused"), get_option("split_f16")
+    try:
+        set_option("split_f16", 1)
+        set_option("fused", 3)
+        assert bench.fused16_used(c3) and bench.tag_products("fvp_fused", c3) == 3
+        assert bench.tag_peak("fvp_fused", c3) == pytest.approx(bench.PEAK_BF16_TFLOPS / 3)
+        assert not bench.fused16_used([4, 64, 2])              # one hidden layer: fused.hip
+        assert bench.tag_products("fvp_fused", [4, 64, 2]) == 6
+        set_option("fused", 2)
+        assert bench.tag_products("fvp_fused", c3) == 6
+        set_option("fused", 3)
+        set_option("split_f16", 0)
+        assert bench.tag_products("fvp_fused", c3) == 6       # fused16 needs the f16 split
+    finally:
+        set_option("fused", saved[0])
+        set_option("split_f16", saved[1])
+    n = 1000
+    assert bench.tag_flops("pg_fused", c3, n) == 2.0 * n * ((64 * 64 + 64 * 18) + (128 * 64 + 64 * 64 + 64 * 18))
+    assert bench.tag_bytes("pg_fused", c3, n) == 4.0 * n * sum(c3)
+    assert bench.tag_is_split("pg_fused", c3) and bench.tag_products("pg_fused", c3) == 3
