@@ -121,6 +121,10 @@ struct trpo_engine {
   // the prepare pass also produced the policy gradient's DS_{L-2} (hbwd.hip, in RD[L-2]); any launch that
   // writes RD clears it
   bool ds_ready = false;
+  // fused16.hip's prepare launch also left the policy gradient's blocks in the first pg_grid slabs; any slab writer
+  // clears it
+  bool pg_ready = false;
+  int pg_grid = 0;
   bool use_hbwd2() const {
     // a hidden layer below the head layer, wider than 128 (one thread per column: at 64 columns three
     // quarters of its lanes idle, and C3 ran 3 % slower than on the row GEMMs); E_{L-2} is written too
@@ -988,9 +992,28 @@ struct trpo_engine {
     // recomputes it from H and D_{L-1}.
     prep_e_top = e_top_needed();
     ds_ready = false;
+    pg_ready = false;
     d1_plane = false;
     d1_tiled = false;
     const bool hb2 = use_hbwd2();
+    if (use_fused16()) {
+      // D_1, E_1, E_0 and the policy gradient's slabs in one launch on the f16 weight images (fused16.hip)
+      fused16_w_images();
+      Fused16Args fa = fused16_args(nullptr, nullptr, pg_grid);
+      fa.D1out = D[1];
+      fa.E1out = E[1];
+      fa.E0out = E[0];
+      fa.am_d1_out = am_d(1);
+      {
+        Scope sp(this, "bwd_pg");
+        launch_prep_pg_fused16(fa, pg_grid, stream);
+        check_launch();
+      }
+      pg_ready = true;
+      reduce_losses(0, nullptr);
+      prepared = true;
+      return;
+    }
     for (int l = L - 1; l >= 1; --l) {
       const bool need_d = l > 1, need_e = l < L - 1 || prep_e_top;
       if (!need_d && !need_e) continue;
@@ -1082,6 +1105,7 @@ struct trpo_engine {
   void wgrad_layer(int l, int nseg, WSeg s0, WSeg s1, int colsum_seg, const int* skip, const char* tag,
                    bool keeps_pg_head = false) {
     if (!keeps_pg_head) ds_ready = false;
+    pg_ready = false;
     WGradArgs a{};
     a.rows = (int)n;
     a.Ma = w[l];
@@ -1109,7 +1133,9 @@ struct trpo_engine {
   void policy_grad() {
     prepare();
     if (use_fused16()) {
-      pg_fused16();
+      if (!pg_ready) pg_fused16();
+      ds_ready = false;
+      reduce_grad(g, nullptr, pg_grid);
       return;
     }
     ensure_w3();
@@ -1166,6 +1192,7 @@ struct trpo_engine {
     if (prepared && e_top_needed() && !prep_e_top) prepared = false;
     prepare();
     ds_ready = false;   // the FVP's R-backward writes RD (DS_{L-2}'s scratch)
+    pg_ready = false;   // ... and every FVP path the slabs
     if (use_fused16()) {
       fvp_fused16(v, out, skip);
       return;
@@ -1472,18 +1499,17 @@ struct trpo_engine {
     allreduce_f32(out, (size_t)P);
   }
 
-  // g in one launch on the same machinery (fused16.hip, PG form): the surr backward from DS_2 and every block of g
+  // g's slabs in one launch on the same machinery (fused16.hip, PG form): the surr backward from DS_2 and every
+  // block of g (when the prepare launch's are gone)
   void pg_fused16() {
     fused16_w_images();
-    int grid = 1;
-    const Fused16Args fa = fused16_args(nullptr, nullptr, grid);
+    const Fused16Args fa = fused16_args(nullptr, nullptr, pg_grid);
     {
       Scope sp(this, "pg_fused");
-      launch_pg_fused16(fa, grid, stream);
+      launch_pg_fused16(fa, pg_grid, stream);
       check_launch();
     }
-    ds_ready = false;
-    reduce_grad(g, nullptr, grid);
+    pg_ready = true;
   }
 
   // the same Hv with the row-local part (R-forward, R-head, R-backward) in one fused launch
@@ -1684,7 +1710,9 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready, d1_plane, d1_tiled;
+    bool prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready, pg_ready, d1_plane,
+        d1_tiled;
+    int pg_grid;
   } upd_flags{};
   void drop_graph() {
     if (upd_exec) {
@@ -1714,6 +1742,8 @@ struct trpo_engine {
       have_returns = upd_flags.have_returns;
       prep_e_top = upd_flags.prep_e_top;
       ds_ready = upd_flags.ds_ready;
+      pg_ready = upd_flags.pg_ready;
+      pg_grid = upd_flags.pg_grid;
       d1_plane = upd_flags.d1_plane;
       d1_tiled = upd_flags.d1_tiled;
       return;
@@ -1750,8 +1780,8 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready,
-                            d1_plane, d1_tiled};
+    upd_flags = PrefixFlags{prepared, w3_valid,   chain_w_valid, f16_w_valid, have_returns, prep_e_top,
+                            ds_ready, pg_ready, d1_plane,      d1_tiled,    pg_grid};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;

@@ -167,9 +167,11 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
 enum { jV0 = 0, jW1, jV1, jW2, jV2, jW2t, jV2t, jW1t, jV1t };
 
 // FW = waves per workgroup, TI0 = 16-feature tiles of obs (1, 2, 4, 8), OTA = 16-action tiles of the head;
-// PG: the policy gradient instead of the FVP (the same machinery on the backward chain alone)
-template <int FW, int LB, int TI0, int OTA, bool PG>
+// MODE: 0 the FVP; 1 the policy gradient instead (the same machinery on the backward chain alone); 2 the policy
+// gradient and, on the same weight chunks, the prepare pass's backward below the head (D_1, E_1, E_0)
+template <int FW, int LB, int TI0, int OTA, int MODE>
 __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16Args fa) {
+  constexpr bool PG = MODE >= 1, PREP = MODE == 2;
   constexpr int OTM = 4;                       // 16-feature tiles of a hidden layer
   constexpr int NT = FW * 64;
   constexpr int CHU = 8 * 16 * OTM;            // 16-B units of a 64-row chunk: 2 planes x 64 rows x 64 B
@@ -228,6 +230,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // near saturation 1 - H^2 is as small as H's own rounding
   f32x4 H2f[OTM], H1f[OTM];
   f32x4 xn0 = z4, xn1 = z4;   // first X chunk of the next group (loaded one group ahead)
+  float mD1 = 0.0f;           // PREP: running max |D_1| of this lane
   const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, 0x7ffffff0, 0x00020000);
   // weight chunks in flight WS ahead, in WS register sets: chunk c of a group sits in set c % WS (the group's
   // chunk count NCH need not be a multiple of WS: the next group's chunk k < WS is loaded into set k by whichever
@@ -384,9 +387,12 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       if constexpr ((FUSED16_ABL & 1) != 0) return f32x4{0.5f, 0.25f, 0.125f, 0.0625f};
       return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0));
     };
+    auto st4 = [&](float* p, int ld, int t, const f32x4& x) {   // acc-layout tile t of this lane's state row
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(cu32x4, x), rsrc(p, ld), voff(ld, t), 0, 0);
+    };
     auto bias4 = [&](int l, int t) -> f32x4 { return *reinterpret_cast<const f32x4*>(&sc[l][16 * t + 4 * g]); };
 
-    auto mma = [&](auto OT_, const fh8 (&b)[2]) __attribute__((always_inline)) {
+    auto mma_to = [&](auto OT_, const fh8 (&b)[2], f32x4 (&ac)[OTM]) __attribute__((always_inline)) {
       constexpr int OT = decltype(OT_)::value;
       constexpr int pl = OT * 512;   // u16 per plane of the chunk
       fh8 f[2], nx[2];
@@ -398,7 +404,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
           for (int p = 0; p < 2; ++p) nx[p] = *reinterpret_cast<const fh8*>(W + p * pl + (ot + 1) * 512);
         }
-        acc[ot] = mfma3(f, b, acc[ot]);
+        ac[ot] = mfma3(f, b, ac[ot]);
         if (ot + 1 < OT) {
 #pragma unroll
           for (int p = 0; p < 2; ++p) f[p] = nx[p];
@@ -406,13 +412,18 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       }
     };
 
+    auto mma = [&](auto OT_, const fh8 (&b)[2]) __attribute__((always_inline)) { mma_to(OT_, b, acc); };
+    auto no_extra = [](int) {};
+
     // One chain step: acc = [S (KC0 chunks, registers, times 2^eS per state) x job jS |
     //                        M1 (KC1 chunks, memory, times sM) x job jS + 1 (jS when KC0 = 0)];
     // acc * su is the f32 value;
-    // the epilogue operand Pre is prefetched into PF; cap (optional) receives M1's split planes.
+    // the epilogue operand Pre is prefetched into PF; cap (optional) receives M1's split planes; extra(c) runs
+    // with chunk c of the step in LDS (more products on the same weights).
     float su = 1.0f;
     auto step = [&](auto OT_, auto KC0_, auto KC1_, int jS, int eS, const float* M1, int ld1, float sM, int eM,
-                    const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre) __attribute__((always_inline)) {
+                    const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre, auto&& extra)
+        __attribute__((always_inline)) {
       constexpr int OT = decltype(OT_)::value, KC0 = decltype(KC0_)::value, KC1 = decltype(KC1_)::value;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -449,6 +460,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
           for (int j = 0; j < KC1; ++j)
             if (KC0 + j >= RING && KC0 + j - RING == c) issue(j);
           mma(OT_, b);
+          extra(c);
         }
         if constexpr (KC1 > 0) {   // segment scales: 2^(ej[jS] + eS) -> 2^(ej[jS + 1] + eM)
           const int d = ej[jS + 1] + eM - ej[jS] - eS;
@@ -466,6 +478,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
         mkb16(mb[c][0], mb[c][1], sM, b);
         if (cap) putb(cap, c, b);
         mma(OT_, b);
+        extra(KC0 + c);
       }
       // (a register-only step leaves its per-state scale: su is then per lane)
       su = KC1 > 0 ? __builtin_ldexpf(1.0f, -(ej[jM] + eM)) : __builtin_amdgcn_ldexpf(1.0f, -(ej[jS] + eS));
@@ -483,26 +496,78 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       //      DS_0 = (DS_1 W_1^T)(1 - H_1^2); g_W_l = H_l^T DS_l (H_0 = X), g_b_l = colsum DS_l.
       //      DS_2 is the head's surr logit delta from the prepare pass. ----
       const float sDS = __builtin_ldexpf(1.0f, eDS);
-      step(C4{}, C0{}, C1{}, jW2t, 0, fa.DS, a.ld[3], sDS, eDS, a.H[2], a.ld[2], OTM, sD, false);
+      // PREP: the KL_ff plain backward on the same chunks, DH_1 = D_2 W_2^T, D_1 = DH_1 (1 - H_2^2),
+      // E_1 = -2 DH_1 H_2, E_0 = -2 (D_1 W_1^T) H_1 (engine.cpp prepare(); D_0 has no reader)
+      f32x4 accD[OTM], D1v[OTM];
+      f32x4 d2c0 = z4, d2c1 = z4;
+      if constexpr (PREP) {
+        const __amdgpu_buffer_rsrc_t rd2 = rsrc(a.D[2], a.ld[3]);
+        d2c0 = ld4(rd2, voff(a.ld[3], 0));
+        d2c1 = ld4(rd2, voff(a.ld[3], 1));
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) accD[t] = z4;
+      }
+      auto extra1 = [&](int) {
+        if constexpr (PREP) {
+          fh8 b[2];
+          mkb16(d2c0, d2c1, sD2, b);
+          mma_to(C4{}, b, accD);
+        }
+      };
+      step(C4{}, C0{}, C1{}, jW2t, 0, fa.DS, a.ld[3], sDS, eDS, a.H[2], a.ld[2], OTM, sD, false, extra1);
       f32x4 DS1[OTM];
+      const float suD = __builtin_ldexpf(1.0f, -(ej[jW2t] + eD2));
 #pragma unroll
       for (int t = 0; t < OTM; ++t) {
         const f32x4 h = PF[t];
 #pragma unroll
         for (int i = 0; i < 4; ++i) DS1[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));
         put4(sA, t, h, sH);   // H_2, the head layer's pass operand (sA is free: past this step's chunk barrier)
+        if constexpr (PREP) {
+          f32x4 e1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float dh = accD[t][i] * suD;
+            D1v[t][i] = dh * c_one_minus_sq(h[i]);
+            e1[i] = -2.0f * dh * h[i];
+          }
+          st4(fa.D1out, a.ld[2], t, D1v[t]);
+          st4(fa.E1out, a.ld[2], t, e1);
+        }
       }
       float mst = state_max<OTM>(DS1);
       wave_max(3, mst);
+      float mstD = 0.0f;
+      if constexpr (PREP) {
+        mstD = state_max<OTM>(D1v);
+        mD1 = fmaxf(mD1, mstD);
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) accD[t] = z4;
+      }
+      const float sD1s = __builtin_ldexpf(1.0f, f16_scale_exp(mstD));
+      auto extra2 = [&](int c) {
+        if constexpr (PREP) {
+          fh8 b[2];
+          mkb16(D1v[2 * c], D1v[2 * c + 1], sD1s, b);
+          mma_to(C4{}, b, accD);
+        }
+      };
 #pragma unroll
       for (int t = 0; t < OTM; ++t) S[t] = DS1[t];
-      step(C4{}, C2{}, C0{}, jW1t, f16_scale_exp(mst), a.H[1], 0, 1.0f, 0, a.H[1], a.ld[1], OTM, nullptr, false);
+      step(C4{}, C2{}, C0{}, jW1t, f16_scale_exp(mst), a.H[1], 0, 1.0f, 0, a.H[1], a.ld[1], OTM, nullptr, false, extra2);
+      const float suD0 = __builtin_amdgcn_ldexpf(1.0f, -(ej[jW1t] + f16_scale_exp(mstD)));
 #pragma unroll
       for (int t = 0; t < OTM; ++t) {
         const f32x4 h = PF[t];
         H1f[t] = h;
 #pragma unroll
         for (int i = 0; i < 4; ++i) S[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));   // DS_0
+        if constexpr (PREP) {
+          f32x4 e0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) e0[i] = -2.0f * (accD[t][i] * suD0) * h[i];
+          st4(fa.E0out, a.ld[1], t, e0);
+        }
       }
       wave_max(4, state_max<OTM>(S));
       const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
@@ -569,7 +634,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
 
     // ---- R-forward: RH_1 = (1 - H_1^2)(X V_0 + c_0) ----
-    step(C4{}, C0{}, CKX{}, jV0, 0, a.X, a.ld[0], sX, eX, a.H[1], a.ld[1], OTM, nullptr, true);
+    step(C4{}, C0{}, CKX{}, jV0, 0, a.X, a.ld[0], sX, eX, a.H[1], a.ld[1], OTM, nullptr, true, no_extra);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
       const f32x4 cb = bias4(0, t), h = PF[t];
@@ -581,7 +646,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     // ---- RH_2 = (1 - H_2^2)(RH_1 W_1 + H_1 V_1 + c_1) ----
 #pragma unroll
     for (int t = 0; t < OTM; ++t) S[t] = RH1[t];
-    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false);
+    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false, no_extra);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
       const f32x4 cb = bias4(1, t), h = PF[t];
@@ -597,7 +662,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       const int A = a.w[3];
 #pragma unroll
       for (int t = 0; t < OTM; ++t) S[t] = RH2[t];
-      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false);
+      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false, no_extra);
       // R-softmax in f32 on the cancellation-free form of tail.hip / gemm.hip kRHead:
       //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k],
       //   Rp = p (Rz - <p, Rz>), A = p / (p + eps), B = eps / (p + eps); the 4 lanes of a state hold 8 actions each
@@ -659,7 +724,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
 
     // ---- R-backward into layer 2's input: RD_1 = (RD_2 W_2^T + D_2 V_2^T)(1 - H_2^2) + E_1 RH_2; D_2 captured ----
-    step(C4{}, C1{}, C1{}, jW2t, f16_scale_exp(mst), a.D[2], a.ld[3], sD2, eD2, a.E[1], a.ld[2], OTM, sD, false);
+    step(C4{}, C1{}, C1{}, jW2t, f16_scale_exp(mst), a.D[2], a.ld[3], sD2, eD2, a.E[1], a.ld[2], OTM, sD, false, no_extra);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
       const f32x4 h = H2f[t], e = PF[t];
@@ -694,7 +759,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
 
     // ---- R-backward into layer 1's input: RD_0 = (RD_1 W_1^T + D_1 V_1^T)(1 - H_1^2) + E_0 RH_1; D_1 captured ----
-    step(C4{}, C2{}, C2{}, jW1t, f16_scale_exp(mst), a.D[1], a.ld[2], sD1, eD1, a.E[0], a.ld[1], OTM, sD, false);
+    step(C4{}, C2{}, C2{}, jW1t, f16_scale_exp(mst), a.D[1], a.ld[2], sD1, eD1, a.E[0], a.ld[1], OTM, sD, false, no_extra);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
       const f32x4 h = H1f[t], e = PF[t];
@@ -752,6 +817,19 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 
   // ---- this workgroup's slab: owned gradient tiles (C layout: rows 4g + r, column s) and biases ----
   __syncthreads();
+  if constexpr (PREP) {   // D_1's running max (kernels.h slots): workgroup max, one atomicMax per workgroup
+    float m = mD1;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) sred[0][wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0 && fa.am_d1_out) {
+      float mm = 0.0f;
+#pragma unroll
+      for (int w = 0; w < FW; ++w) mm = fmaxf(mm, sred[0][w]);
+      if (mm > 0.0f) atomicMax(fa.am_d1_out + (blockIdx.x % kAmaxSub) * kAmaxStride, __float_as_uint(mm));
+    }
+  }
   const int lane = threadIdx.x & 63, g = lane >> 4, s = lane & 15;
   float* out = fa.f.slab + (size_t)blockIdx.x * fa.f.slab_stride;
   auto wout = [&](auto& dacc, int m, int TI, int TJ) __attribute__((always_inline)) {
@@ -787,28 +865,30 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 
 int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
 
-template <int TI0, bool PG>
+template <int TI0, int MODE>
 void launch_ti0(const Fused16Args& a, int grid, hipStream_t s) {
   constexpr int FW = FUSED16_FW, LB = FUSED16_LB;
   if (a.f.c.w[3] <= 16)
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1, PG>), dim3(grid), dim3(FW * 64), 0, s, a);
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1, MODE>), dim3(grid), dim3(FW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2, PG>), dim3(grid), dim3(FW * 64), 0, s, a);
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2, MODE>), dim3(grid), dim3(FW * 64), 0, s, a);
 }
 
-template <bool PG>
+template <int MODE>
 void launch_fused16(const Fused16Args& a, int grid, hipStream_t s) {
+  constexpr bool PG = MODE >= 1;
   if (grid <= 0) return;
   if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16: unsupported shape");
   if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16: chunk table");
   const int rb = fused16_states_per_group();
   if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16: group count does not match");
   if (PG && !a.DS) throw std::runtime_error("fused16 policy gradient: no head delta");
+  if (MODE == 2 && (!a.D1out || !a.E1out || !a.E0out)) throw std::runtime_error("fused16 prepare backward: no outputs");
   switch (ti0_of(a.f.c.w[0])) {
-    case 1: launch_ti0<1, PG>(a, grid, s); break;
-    case 2: launch_ti0<2, PG>(a, grid, s); break;
-    case 4: launch_ti0<4, PG>(a, grid, s); break;
-    default: launch_ti0<8, PG>(a, grid, s); break;
+    case 1: launch_ti0<1, MODE>(a, grid, s); break;
+    case 2: launch_ti0<2, MODE>(a, grid, s); break;
+    case 4: launch_ti0<4, MODE>(a, grid, s); break;
+    default: launch_ti0<8, MODE>(a, grid, s); break;
   }
 }
 
@@ -834,7 +914,8 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
   hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
 }
 
-void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<false>(a, grid, s); }
-void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<true>(a, grid, s); }
+void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<0>(a, grid, s); }
+void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<1>(a, grid, s); }
+void launch_prep_pg_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<2>(a, grid, s); }
 
 }  // namespace trpo

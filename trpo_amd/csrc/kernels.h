@@ -396,6 +396,10 @@ struct Fused16Args {
   const unsigned* am_d2;
   const float* DS;                   // policy gradient only: the head's surr logit delta DS_2 [n][ld 3] and its slot
   const unsigned* am_ds2;
+  float* D1out;                      // with the prepare backward (launch_prep_pg_fused16): D_1, E_1 [n][ld 2], E_0
+  float* E1out;                      // [n][ld 1] and D_1's running-max slot
+  float* E0out;
+  unsigned* am_d1_out;
 };
 bool fused16_eligible(int L, const int* w);
 int fused16_obs_chunks(int obs);     // 32-deep k-chunks of V_0's image (obs rounded to 32, 64 or 128)
@@ -407,6 +411,9 @@ void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s);
 // The policy gradient of the same shapes in one launch (fused16.hip, PG form): DS_1, DS_0 by the backward chain
 // over W_2^T / W_1^T's image chunks and g's blocks H_l^T DS_l + colsum DS_l into the slabs, as the FVP's.
 void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
+// ... and with it, on the same weight chunks, the prepare pass's backward below the head: D_1, E_1, E_0 and D_1's
+// running max (engine.cpp prepare())
+void launch_prep_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
