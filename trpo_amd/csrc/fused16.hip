@@ -45,6 +45,10 @@
 #ifndef FUSED16_WSETS
 #define FUSED16_WSETS 2   // weight chunks in flight (register sets)
 #endif
+#ifndef FUSED16_REUSE
+#define FUSED16_REUSE 1   // H_1 / H_2 tiles loaded once per group and reused as later steps' memory segments (1), and
+                          // H_1 also for the layer-1 pass and R-backward epilogue (2); 0: each step loads its own
+#endif
 #ifndef FUSED16_PFEARLY
 #define FUSED16_PFEARLY 1   // 1: a step's epilogue operand is loaded before its register segment, not its memory one
 #endif
@@ -422,8 +426,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     // with chunk c of the step in LDS (more products on the same weights).
     float su = 1.0f;
     auto step = [&](auto OT_, auto KC0_, auto KC1_, int jS, int eS, const float* M1, int ld1, float sM, int eM,
-                    const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre, auto&& extra)
-        __attribute__((always_inline)) {
+                    const float* Pre, int ldp, int OTp, unsigned short* cap, bool pre, auto&& extra,
+                    const f32x4* Mreg = nullptr) __attribute__((always_inline)) {
       constexpr int OT = decltype(OT_)::value, KC0 = decltype(KC0_)::value, KC1 = decltype(KC1_)::value;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -432,7 +436,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       // memory chunk j (step chunk KC0 + j) is loaded RING chunks ahead of its use, or at the step's start
       f32x4 mb[KC1 > 0 ? KC1 : 1][2];
       auto issue = [&](int j) {
-        if (j == 0 && pre) {   // X's first chunk, loaded during the previous group
+        if (Mreg) {            // M1 already in registers (acc-layout tiles 2j, 2j + 1)
+          mb[j][0] = Mreg[2 * j];
+          mb[j][1] = Mreg[2 * j + 1];
+        } else if (j == 0 && pre) {   // X's first chunk, loaded during the previous group
           mb[0][0] = xn0;
           mb[0][1] = xn1;
         } else {
@@ -640,13 +647,15 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       const f32x4 cb = bias4(0, t), h = PF[t];
 #pragma unroll
       for (int i = 0; i < 4; ++i) RH1[t][i] = c_one_minus_sq(h[i]) * __builtin_fmaf(acc[t][i], su, cb[i]);
+      H1f[t] = h;   // H_1: the next step's memory segment (FUSED16_REUSE)
     }
     float mst = state_max<OTM>(RH1);
     wave_max(0, mst);
     // ---- RH_2 = (1 - H_2^2)(RH_1 W_1 + H_1 V_1 + c_1) ----
 #pragma unroll
     for (int t = 0; t < OTM; ++t) S[t] = RH1[t];
-    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false, no_extra);
+    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false, no_extra,
+         FUSED16_REUSE ? H1f : nullptr);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
       const f32x4 cb = bias4(1, t), h = PF[t];
@@ -662,7 +671,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       const int A = a.w[3];
 #pragma unroll
       for (int t = 0; t < OTM; ++t) S[t] = RH2[t];
-      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false, no_extra);
+      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false, no_extra,
+           FUSED16_REUSE ? H2f : nullptr);
       // R-softmax in f32 on the cancellation-free form of tail.hip / gemm.hip kRHead:
       //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k],
       //   Rp = p (Rz - <p, Rz>), A = p / (p + eps), B = eps / (p + eps); the 4 lanes of a state hold 8 actions each
@@ -685,7 +695,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       float spB = 0.0f, sRAB = 0.0f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        inv[k] = 1.0f / (pf[k] + kEps);
+        inv[k] = __builtin_amdgcn_rcpf(pf[k] + kEps);   // v_rcp_f32 (1 ulp): A and B need no IEEE quotient
         const float Rp = pf[k] * (zf[k] - prz);
         const float Aa = pf[k] * inv[k], B = kEps * inv[k];
         spB += pf[k] * B;
@@ -742,7 +752,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       for (int t = 0; t < OTM; ++t) put4(sA, t, RH2[t], sg);
       const __amdgpu_buffer_rsrc_t rn = rsrc(a.H[1], a.ld[1]);
 #pragma unroll
-      for (int t = 0; t < OTM; ++t) H1f[t] = ld4(rn, voff(a.ld[1], t));
+      for (int t = 0; t < OTM; ++t)
+        if (FUSED16_REUSE < 2) H1f[t] = ld4(rn, voff(a.ld[1], t));
       lds_barrier();
       run(dwl, C4{}, COTA{}, 0, eg + eD2);
       // (Hv)_W_1 += H_1^T RD_1

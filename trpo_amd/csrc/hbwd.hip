@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
         float spB = 0.0f, rest = 0.0f;
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
-          const float Bj = j < a.A ? kEps / (p[j] + kEps) : 0.0f;
+          const float Bj = j < a.A ? kEps * __builtin_amdgcn_rcpf(p[j] + kEps) : 0.0f;   // O(eps) term: 1-ulp rcp
           spB += p[j] * Bj;
           rest += (j < a.A && j != av) ? p[j] : 0.0f;
         }
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
             const bool real = j < a.A;
             float pd = p[j];
             asm volatile("" : "+v"(pd));   // recomputed, not kept from the first loop
-            const float Bj = real ? kEps / (pd + kEps) : 0.0f;
+            const float Bj = real ? kEps * __builtin_amdgcn_rcpf(pd + kEps) : 0.0f;
             const float dl = real ? pd * invN * (Bj - spB) : 0.0f;
             const float ds = real ? coef * (j == av ? rest : -pd) : 0.0f;
             Pr[j] = real ? p[j] : 0.0f;

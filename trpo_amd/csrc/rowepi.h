@@ -292,7 +292,11 @@ __device__ __forceinline__ void epi_row(const RowEpiArgs& e, int row, bool rowva
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         const T pd = p[t];
+#if TRPO_PREP_HEAD64
         B[t] = real[t] ? (T)kEps / (pd + (T)kEps) : T(0);
+#else
+        B[t] = real[t] ? kEps * __builtin_amdgcn_rcpf(pd + kEps) : 0.0f;   // O(eps) term: 1-ulp v_rcp_f32
+#endif
         spBp += pd * B[t];
         restp += (real[t] && 32 * t + lr != a) ? pd : T(0);
       }
