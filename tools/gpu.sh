@@ -11,7 +11,8 @@
 #   bash tools/gpu.sh prof <name> [bench args]          rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes
 #   bash tools/gpu.sh sq <name> [bench args]            SQ / GRBM counter passes per kernel (pmc_kernels.sh)
 #   bash tools/gpu.sh round <name>                      tests + smoke + C4 (with CPU baseline) / C3 / C2 / C5 lines
-#   bash tools/gpu.sh final <name>                      round + prof
+#   bash tools/gpu.sh rehearsal <name>                  2-rank rehearsal line on the one GPU (rank digest check)
+#   bash tools/gpu.sh final <name>                      round + rehearsal + prof
 # Several steps: bash tools/gpu.sh chain <name> "tests" "bench c4 c3" "prof" ...  (each a sub-command above
 # without its <name>)
 set -o pipefail
@@ -69,8 +70,14 @@ case $CMD in
     python tools/pmc_summary.py gpurun_out/$NAME > $OUT/sq_counters.txt 2>&1; tail -3 $OUT/sq_counters.txt ;;
   round)
     bash tools/gpu.sh tests $NAME && bash tools/gpu.sh smoke $NAME && bash tools/gpu.sh bench $NAME c4 c3 c2 c5 ;;
+  rehearsal)   # 2 ranks sharing the one GPU (host all-reduce): the launcher and the per-rank digest check
+    timeout -k 10 600 python -u bench.py --gpus 2 --rehearsal --rows 400000 --steps 3 --warmup 1 --no-cpu-baseline \
+      --no-alt > $OUT/bench_2rank_rehearsal.json 2> $OUT/bench_2rank_rehearsal.err || { tail -5 $OUT/bench_2rank_rehearsal.err; exit 1; }
+    python -c "
+import json; d=json.loads(open('$OUT/bench_2rank_rehearsal.json').read().strip().splitlines()[-1])
+print('rehearsal', d['value'], d['comm'].get('transport'), d['comm'].get('ranks'), d['comm'].get('ranks_bitwise_equal'))" ;;
   final)
-    bash tools/gpu.sh round $NAME && bash tools/gpu.sh prof $NAME --steps 3 --warmup 1 --no-alt ;;
+    bash tools/gpu.sh round $NAME && bash tools/gpu.sh rehearsal $NAME && bash tools/gpu.sh prof $NAME --steps 3 --warmup 1 --no-alt ;;
   chain)
     for step in "$@"; do
       set -- $step
