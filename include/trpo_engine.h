@@ -214,8 +214,8 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * rbwd0 (or E_{L-2} where the FVP path reads it) and the policy gradient's head-layer weight gradient;
  * <= 32 actions, last hidden width 129..256; 2 = on f32 MFMA, the default; 1 = on VALU f32 FMA chains),
  * "head_fwd" (softmax head forwards with one state per lane on f32 FMAs,
- * hbwd.hip: 1 = the prepare and the line-search heads; 2 = the line-search heads, and the prepare head
- * when the head has <= 8 actions, the default; 0 = off), "splits" (split-K slabs of the FVP's weight
+ * hbwd.hip: 1 = the prepare and the line-search heads, the default; 2 = the line-search heads, and the
+ * prepare head when the head has <= 8 actions; 0 = off), "splits" (split-K slabs of the FVP's weight
  * gradients; 0 = auto: by tile count, at least one per 16k rows; 512 at C4, 245 at C5) and "pg_splits" (the
  * policy gradient's; 0 = auto: 4 x splits or one per 4k rows, up to 2048): both are read when an engine
  * is created.

@@ -285,7 +285,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"rbwd0": 0}, {"rbwd0": 0, "chain": 0},                   # per-layer R-backward + layer-0 weight gradient
     {"hbwd2": 0}, {"hbwd2": 0, "chain": 0},                   # separate head backwards (prepare / policy gradient)
     {"hbwd2": 1},                                             # the dual head backward on VALU fmaf chains
-    {"head_fwd": 0}, {"head_fwd": 1}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
+    {"head_fwd": 0}, {"head_fwd": 2}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
     {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):

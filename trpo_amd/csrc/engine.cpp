@@ -884,8 +884,8 @@ struct trpo_engine {
       a.seg[0].amaxA = l == 0 ? am_x() : nullptr;   // hidden activations are tanh outputs, |h| <= 1
       a.seg[0].amaxB = &wf == &WFt ? am_wt(l) : am_w(l);
       if (l == 0 && planes_l0()) attach_x_planes(a.seg[0], wf3[0], W0b);
-      // head_fwd 1: the prepare and the loss heads; 2: the loss heads, and the prepare head for <= 8 actions (its
-      // row epilogue is cheap there; at 18 actions the row GEMM's 32-lane head is faster: DESIGN.md §4)
+      // head_fwd 1 (default): the prepare and the loss heads (the prepare outputs leave through LDS as coalesced
+      // rows: C4 3.6 -> 3.1 ms); 2: the loss heads, and the prepare head for <= 8 actions
       const int hfo = g_options.head_fwd;
       const bool prep_hf = hfo == 1 || (hfo == 2 && w[L] <= 8);
       if (l == L - 1 && (hfo == 1 || hfo == 2) && head_fwd_eligible(w[L], w[L - 1]) &&

@@ -451,10 +451,17 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
         }
       }
     }
+    // the row's softmax, loss terms and (PREP) the values its P / D / DS rows are made of; threads past the tile's
+    // rows keep zeros
+    float p[AT];
+    float spB = 0.0f, rest = 0.0f, coef = 0.0f;
+    int av = -1;
+#pragma unroll
+    for (int j = 0; j < AT; ++j) p[j] = 0.0f;
     if (t < nr) {
       const int64_t row = t0 + t;
       const float* oldr = a.old + row * a.Apad;
-      float z[AT], p[AT];
+      float z[AT];
       float zm = -INFINITY;
 #pragma unroll
       for (int j = 0; j < AT; ++j) {
@@ -469,7 +476,7 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
       }
 #pragma unroll
       for (int j = 0; j < AT; ++j) p[j] = p[j] / es;
-      const int av = a.act[row];
+      av = a.act[row];
       const float adv = a.adv[row];
       float pa = 0.0f, olda = 0.0f;
       float klp = 0.0f, enp = 0.0f;
@@ -495,34 +502,48 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
       if constexpr (PREP) {
         // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps); surr logit delta
         // -(adv/(N old_a)) p_a (1[j=a] - p_j)  (gemm.hip kPrepHead), in f32 as there
-        // (B_j is recomputed in the output loop instead of held: AT more VGPRs)
-        const float invN = (float)a.invN;
-        float spB = 0.0f, rest = 0.0f;
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
           const float Bj = j < a.A ? kEps * __builtin_amdgcn_rcpf(p[j] + kEps) : 0.0f;   // O(eps) term: 1-ulp rcp
           spB += p[j] * Bj;
           rest += (j < a.A && j != av) ? p[j] : 0.0f;
         }
-        const float coef = -adv * invN / olda * pa;
-        float* Pr = a.P + row * a.Apad;
-        float* Dr = a.D + row * a.Apad;
-        float* Sr = a.DS + row * a.Apad;
+        coef = -adv * (float)a.invN / olda * pa;
+      }
+    }
+    if constexpr (PREP) {
+      // P, D_L, DS_L through LDS (sH is free after the chunk loop): each thread's row into a [row][AT + 1] image,
+      // then the tile's rows -- contiguous in HBM -- stored by consecutive threads.  A row per lane written
+      // directly is 64 scattered 80-B pieces per store instruction (round 4: 5.2 vs 3.9 ms for the row GEMM head).
+      float* so = sH;
+      constexpr int ldo = AT + 1;
+      static_assert(ldo <= kHfLd, "head_fwd staging");
+      const float invN = (float)a.invN;
+#pragma unroll
+      for (int kind = 0; kind < 3; ++kind) {
+        __syncthreads();   // the chunk loop's (or the previous kind's) reads of sH are done
 #pragma unroll
         for (int j = 0; j < AT; ++j) {
-          if (j < a.Apad) {
-            const bool real = j < a.A;
-            float pd = p[j];
-            asm volatile("" : "+v"(pd));   // recomputed, not kept from the first loop
+          const bool real = j < a.A;
+          const float pd = p[j];
+          float v;
+          if (kind == 0) {
+            v = real ? pd : 0.0f;
+          } else if (kind == 1) {
             const float Bj = real ? kEps * __builtin_amdgcn_rcpf(pd + kEps) : 0.0f;
-            const float dl = real ? pd * invN * (Bj - spB) : 0.0f;
-            const float ds = real ? coef * (j == av ? rest : -pd) : 0.0f;
-            Pr[j] = real ? p[j] : 0.0f;
-            Dr[j] = dl;
-            Sr[j] = ds;
-            mD = fmaxf(mD, fabsf(dl));
-            mS = fmaxf(mS, fabsf(ds));
+            v = real ? pd * invN * (Bj - spB) : 0.0f;
+            mD = fmaxf(mD, fabsf(v));
+          } else {
+            v = real ? coef * (j == av ? rest : -pd) : 0.0f;
+            mS = fmaxf(mS, fabsf(v));
           }
+          so[t * ldo + j] = v;
+        }
+        __syncthreads();
+        float* dst = (kind == 0 ? a.P : kind == 1 ? a.D : a.DS) + t0 * AT;   // Apad == AT
+        for (int i = t; i < nr * AT; i += kHfRows) {
+          const int r = i / AT, c = i - r * AT;
+          dst[i] = so[r * ldo + c];
         }
       }
     }

@@ -35,8 +35,8 @@ struct Options {
                    // launch that reads H once (hbwd.hip), with D_1's hi plane under rbwd0: 0 off, 1 on VALU fmaf
                    // chains, 2 (default) on f32 MFMA
   int head_fwd;    // engine: softmax head forwards with one state per lane on f32 FMAs (hbwd.hip) instead of the
-                   // f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 prepare + line search, 2 line
-                   // search, and the prepare head when the head has <= 8 actions
+                   // f32 MFMA row GEMM with its 32-lane row epilogue: 0 off, 1 (default) prepare + line search,
+                   // 2 line search, and the prepare head when the head has <= 8 actions
   int splits;      // engine: weight-gradient split-K slabs of the FVP launches (0 = auto: 512 at C4)
   int pg_splits;   // engine: the policy gradient's split-K slabs (0 = auto: 4 x splits, at most 2048)
 };
