@@ -451,6 +451,8 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
         }
       }
     }
+    constexpr int ldo = AT + 1;   // [row][AT + 1] images in sH (free after the chunk loop)
+    static_assert(ldo <= kHfLd, "head_fwd row images");
     // the row's softmax, loss terms and (PREP) the values its P / D / DS rows are made of; threads past the tile's
     // rows keep zeros
     float p[AT];
@@ -516,8 +518,6 @@ __global__ void __launch_bounds__(kHfRows, PREP ? (AT <= 20 ? 3 : 2) : (AT <= 28
       // then the tile's rows -- contiguous in HBM -- stored by consecutive threads.  A row per lane written
       // directly is 64 scattered 80-B pieces per store instruction (round 4: 5.2 vs 3.9 ms for the row GEMM head).
       float* so = sH;
-      constexpr int ldo = AT + 1;
-      static_assert(ldo <= kHfLd, "head_fwd staging");
       const float invN = (float)a.invN;
 #pragma unroll
       for (int kind = 0; kind < 3; ++kind) {
