@@ -12,7 +12,8 @@
 #   bash tools/gpu.sh sq <name> [bench args]            SQ / GRBM counter passes per kernel (pmc_kernels.sh)
 #   bash tools/gpu.sh round <name>                      tests + smoke + C4 (with CPU baseline) / C3 / C2 / C5 lines
 #   bash tools/gpu.sh rehearsal <name>                  2-rank rehearsal line on the one GPU (rank digest check)
-#   bash tools/gpu.sh final <name>                      round + rehearsal + prof
+#   bash tools/gpu.sh rccl <name>                       C4 line at one rank through a one-rank RCCL communicator
+#   bash tools/gpu.sh final <name>                      round + rehearsal + rccl + prof
 # Several steps: bash tools/gpu.sh chain <name> "tests" "bench c4 c3" "prof" ...  (each a sub-command above
 # without its <name>)
 set -o pipefail
@@ -76,8 +77,12 @@ case $CMD in
     python -c "
 import json; d=json.loads(open('$OUT/bench_2rank_rehearsal.json').read().strip().splitlines()[-1])
 print('rehearsal', d['value'], d['comm'].get('transport'), d['comm'].get('ranks'), d['comm'].get('ranks_bitwise_equal'))" ;;
+  rccl)   # every all-reduce through RCCL at world 1 (the N>1 code path minus the peers)
+    timeout -k 10 600 python -u bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-alt --rccl-world1 \
+      > $OUT/bench_c4_rccl1.json 2> $OUT/bench_c4_rccl1.err || { tail -5 $OUT/bench_c4_rccl1.err; exit 1; }
+    summ $OUT/bench_c4_rccl1.json c4-rccl1 ;;
   final)
-    bash tools/gpu.sh round $NAME && bash tools/gpu.sh rehearsal $NAME && bash tools/gpu.sh prof $NAME --steps 3 --warmup 1 --no-alt ;;
+    bash tools/gpu.sh round $NAME && bash tools/gpu.sh rehearsal $NAME && bash tools/gpu.sh rccl $NAME && bash tools/gpu.sh prof $NAME --steps 3 --warmup 1 --no-alt ;;
   chain)
     for step in "$@"; do
       set -- $step
