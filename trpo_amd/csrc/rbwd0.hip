@@ -39,6 +39,13 @@ namespace {
 #ifndef R0_EC
 #define R0_EC 4      // epilogue chunk: accumulator registers per load batch
 #endif
+#ifndef R0_ELA
+#define R0_ELA 2     // epilogue chunks of loads in flight ahead of the one being applied (two segments: H, E, RH;
+                     // 3 spill 25 VGPRs). C4 A/B (profiles/r5ela): 1 -> 2 10.58 -> 10.49 ms
+#endif
+#ifndef R0_ELA1
+#define R0_ELA1 6    // the same for one segment (policy gradient: H only): 2 -> 6 6.76 -> 6.67 ms (profiles/r5pgla)
+#endif
 #ifndef R0_NW
 #define R0_NW 8      // waves per workgroup
 #endif
@@ -424,9 +431,9 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
         return __builtin_amdgcn_make_buffer_rsrc((void*)(p + (size_t)t0 * Npad), 0, tb, 0x00020000);
       };
       const __amdgpu_buffer_rsrc_t rH = mk(A.H), rE = mk(kE ? A.E : A.H), rRH = mk(kE ? A.RH : A.H);
-      // chunks of EC registers of one accumulator tile, the next chunk's loads in flight
-      constexpr int EC = R0_EC;
-      float pre[2][3][EC];
+      // chunks of EC registers of one accumulator tile, the next LA chunks' loads in flight
+      constexpr int EC = R0_EC, LA = kE ? R0_ELA : R0_ELA1;
+      float pre[LA + 1][3][EC];
       auto load_part = [&](int c, float (&d)[3][EC]) {
         constexpr int PPT = 16 / EC;   // chunks per accumulator tile
         const int tn = c % CT, tm = (c / CT) / PPT, hf = (c / CT) % PPT;
@@ -451,11 +458,12 @@ __device__ __forceinline__ void rbwd0_body(const RBwd0Args& A, unsigned short* s
         }
       };
       constexpr int NC = (16 / EC) * TM * CT;
-      load_part(0, pre[0]);
+#pragma unroll
+      for (int c = 0; c < LA && c < NC; ++c) load_part(c, pre[c]);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        if (c + 1 < NC) load_part(c + 1, pre[(c + 1) & 1]);
-        const float (&op)[3][EC] = pre[c & 1];
+        if (c + LA < NC) load_part(c + LA, pre[(c + LA) % (LA + 1)]);
+        const float (&op)[3][EC] = pre[c % (LA + 1)];
         const int tn = c % CT, tm = (c / CT) / (16 / EC), hf = (c / CT) % (16 / EC);
 #pragma unroll
         for (int j = 0; j < EC; ++j) {
