@@ -29,9 +29,16 @@ __device__ __forceinline__ void csplit(float x, unsigned short& h, unsigned shor
 constexpr int kFI = 64;   // features per image row (one pass operand: up to 4 tiles of 16)
 
 // 32-B chunk (one 16-feature tile) of image row r: tile ^ fswz(r).  The 8 rows a half-wave's
-// transposed read touches (r0 + {0..3, 8..11}) then cover all 64 banks once.
+// transposed read touches (r0 + {0..3, 8..11}) then cover all 64 banks once.  Within the chunk, the 8-B unit
+// of features 4u..4u+3 sits at u ^ fsub(r): fswz takes row bits 1 and 3, fsub bits 0 and 2, so the 16
+// consecutive rows of an image store (lane = row, one unit each: ds_write_b64) land on 16 distinct units of
+// the 128-B bank window (round 5: 4-way conflicts before, 34 % of the fused FVP's LDS cycles), while a
+// transposed read still takes one whole chunk per row.
 __device__ __forceinline__ int fswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
-__device__ __forceinline__ int fimg(int r, int f) { return r * kFI + ((((f >> 4) ^ fswz(r))) << 4) + (f & 15); }
+__device__ __forceinline__ int fsub(int r) { return (r & 1) | (((r >> 2) & 1) << 1); }
+__device__ __forceinline__ int fimg(int r, int f) {
+  return r * kFI + ((((f >> 4) ^ fswz(r))) << 4) + (((((f >> 2) & 3) ^ fsub(r))) << 2) + (f & 3);
+}
 
 // 16-B chunk position of k-group g in image row o: g ^ chain_hsw(o).  Makes the
 // 16-lane groups of a ds_read_b128 (MI355X_MICROARCH.md, LDS table) hit 16

@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(FW * 64, FUSED_LB) fvp_fused_kernel(const Fuse
         for (int t = 0; t < 2; ++t) {
           const int r = 32 * ks + 8 * g + 4 * t + tq;
           const fs4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) fs4*)(slot + p * PL + r * kFI + (((ft ^ fswz(r))) << 4) + 4 * tp));
+              (__attribute__((address_space(3))) fs4*)(slot + p * PL + fimg(r, 16 * ft + 4 * tp)));
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[4 * t + e] = x[e];
         }
