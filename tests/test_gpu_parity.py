@@ -287,6 +287,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"hbwd2": 1},                                             # the dual head backward on VALU fmaf chains
     {"head_fwd": 0}, {"head_fwd": 2}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
     {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
+    {"ls_fused": 0},                                          # the line search's per-layer forward on fused16 shapes
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -295,7 +296,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
                                            "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
-                                           "splits", "pg_splits")}
+                                           "splits", "pg_splits", "ls_fused")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -337,6 +338,45 @@ def test_kernel_variants_parity(gpu_available, opts):
     finally:
         for k, v in defaults.items():
             set_option(k, v)
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (11, [64, 64], 3, 3001),           # C2 dims, a partial last 16-state group
+    (128, [64, 64], 18, 100_000),      # C3 dims, many groups per wave
+    (40, [64, 49], 32, 777),           # 4 obs tiles, a partial hidden tile, two action tiles
+    (20, [56, 64], 17, 1),             # one state
+    (64, [64, 64], 16, 40_000),        # two obs chunks, one action tile exactly full
+])
+def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
+    """The line-search loss forward in one launch (fused16.hip fwd_loss16, ls_fused = 1) at a trial theta against
+    the float64 oracle and the per-layer forward (ls_fused = 0): surr / kl / ent of trpo_inksci.py:46-53 through
+    loss() (:127-129)."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=n + 5)
+    rs = np.random.RandomState(n + 6)
+    trial = (dd["theta"] + 0.02 * rs.standard_normal(spec.n_params)).astype(np.float32)
+    ref = O.losses(trial.astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    saved = get_option("ls_fused")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("ls_fused", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            out[mode] = e.eval_losses(trial).astype(np.float64)
+            out[(mode, "again")] = e.eval_losses(trial).astype(np.float64)
+            e.close()
+    finally:
+        set_option("ls_fused", saved)
+    for mode in (1, 0):
+        got = out[mode]
+        assert got[0] == pytest.approx(ref[0], rel=REL, abs=1e-7), (mode, got, ref)
+        assert got[1] == pytest.approx(ref[1], rel=REL, abs=1e-7), (mode, got, ref)
+        assert got[2] == pytest.approx(ref[2], rel=REL), (mode, got, ref)
+        assert np.array_equal(out[mode], out[(mode, "again")])   # deterministic
 
 
 @pytest.mark.parametrize("obs,hidden,A,n", [

@@ -184,6 +184,12 @@ struct trpo_engine {
   int f16_nchunks = 0;
   bool f16_w_valid = false;     // theta parts of the f16 images match theta
   ChainImgArgs f16_jobs{};
+  // the line-search loss forward's images (W_0 | W_1 | W_2 of the trial vector, fwd_loss16)
+  uint16_t* f16_limg = nullptr;
+  int* f16_ltab = nullptr;
+  int* f16_le = nullptr;
+  int f16_lnchunks = 0;
+  ChainImgArgs f16_ljobs{};
   bool use_fused16() const { return g_options.fused == 3 && f16 && f16_img && fused16_eligible(L, w.data()); }
   // layer 1's R-backward (and the policy gradient's backward into layer 0) fused with layer 0's weight
   // gradient (rbwd0.hip): f16 split with X's planes, obs <= 128, first hidden width <= 256
@@ -502,10 +508,11 @@ struct trpo_engine {
     std::vector<int> tab;
     int64_t off16 = 0;
     int nj = 0;
+    ChainImgArgs* jobs = &f16_jobs;
     auto seg = [&](int l, int trans, int which) {
       const int K = trans ? w[l + 1] : w[l], O = trans ? w[l] : w[l + 1];
       const int kc = l == 0 ? fused16_obs_chunks(w[0]) : (K + 31) / 32, otp = (O + 15) / 16 * 16, csz = otp * 8;
-      ChainImgJob& j = f16_jobs.job[nj++];
+      ChainImgJob& j = jobs->job[nj++];
       j.src_off = offW[l];
       j.dst_off = off16 * 8;
       j.K = K;
@@ -540,6 +547,20 @@ struct trpo_engine {
     HIPCHECK(hipMemcpyAsync(f16_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));   // `tab` is a local vector
     f16_nchunks = (int)(tab.size() / 2);
+    // the loss forward's W_0 | W_1 | W_2 (from the trial vector: which = 0, built per line-search trial)
+    tab.clear();
+    off16 = 0;
+    nj = 0;
+    jobs = &f16_ljobs;
+    for (int l = 0; l < L; ++l) seg(l, 0, 0);
+    f16_ljobs.n = nj;
+    f16_limg = dalloc<uint16_t>((size_t)off16 * 8);
+    f16_ltab = dalloc<int>(tab.size());
+    f16_le = dalloc<int>(nj);
+    f16_ljobs.img = f16_limg;
+    HIPCHECK(hipMemcpyAsync(f16_ltab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    f16_lnchunks = (int)(tab.size() / 2);
   }
 
   PolicyShape policy_shape() const {
@@ -1580,6 +1601,39 @@ struct trpo_engine {
   // loss(th) at a device parameter vector, without touching the prepared cache
   void eval_losses_dev(const float* th) {
     require_batch();
+    if (use_fused16() && g_options.ls_fused != 0) {
+      // one launch from the trial vector's f16 images (fused16.hip fwd_loss16_kernel)
+      {
+        Scope sp(this, "ls_img");
+        launch_fused16_img(f16_ljobs, th, nullptr, 0, nullptr, f16_le, stream);
+        check_launch();
+      }
+      FwdLoss16Args la{};
+      la.n = n;
+      for (int l = 0; l <= L; ++l) {
+        la.w[l] = w[l];
+        la.ld[l] = wp[l];
+      }
+      la.X = X;
+      la.theta = th;
+      for (int l = 0; l < L; ++l) la.offb[l] = offb[l];
+      la.img = f16_limg;
+      la.tab = f16_ltab;
+      la.nchunks = f16_lnchunks;
+      la.img_e = f16_le;
+      la.am_x = am_x();
+      la.old = old;
+      la.act = act;
+      la.adv = adv32;
+      la.rowterms = rowterms;
+      {
+        Scope sp(this, "ls_fwd");
+        launch_fwd_loss16(la, num_cus, stream);
+        check_launch();
+      }
+      reduce_losses(1, nullptr);
+      return;
+    }
     PackArgs pa = pack_args(WFt, nullptr, 2);
     launch_pack(pa, th, 0, nullptr, stream);
     split_parts(true, false, false, false, WFt, WFt3, nullptr, "split_t");
@@ -2621,6 +2675,7 @@ static int* option_slot(const std::string& k) {
   if (k == "head_fwd") return &g_options.head_fwd;
   if (k == "splits") return &g_options.splits;
   if (k == "pg_splits") return &g_options.pg_splits;
+  if (k == "ls_fused") return &g_options.ls_fused;
   throw ArgError("unknown option " + k);
 }
 

@@ -874,6 +874,188 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Line-search loss forward (trpo_inksci.py:38-53 at the trial theta, utils.py:170-182 through loss()):
+// X -> tanh(X W_0 + b_0) -> tanh(H_1 W_1 + b_1) -> softmax(H_2 W_2 + b_2) -> the row terms (surr, kl, ent)
+// that reduce_losses sums, for the fused16 shapes.  No weight stream and no barrier in the loop: the three
+// trial weight images (KX + 4 chunks, <= 64 KB) are copied to LDS once per workgroup, and every wave runs its
+// own 16 states through the three layers in accumulator layout (the FVP chain's forward steps with W in place
+// of V), with the next group's X in flight behind the current group's math.  Products as the FVP: scaled f16
+// hi + lo, 3 products; H's scale fixed, X's from its running max, each weight image's from its builder.
+// The head: f32 softmax and logs, as the row GEMM's kLossHead (rowepi.h), over the state's 4 lanes.
+// ---------------------------------------------------------------------------------------------------------
+#ifndef FWDL16_NW
+#define FWDL16_NW 4   // waves per workgroup (sharing one LDS copy of the weights)
+#endif
+template <int TI0, int OTA>
+__global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const FwdLoss16Args a) {
+  constexpr int OTM = 4, KX = (TI0 + 1) / 2, NW = FWDL16_NW, NT = 64 * NW;
+  constexpr int NCK = KX + 4;                  // W_0 (KX chunks), W_1 (2), W_2 (2)
+  constexpr int CHU = 8 * 16 * OTM;            // 16-B units of a full chunk
+  __shared__ cu32x4 wl[NCK][CHU];
+  __shared__ __attribute__((aligned(16))) float sbias[3][64];
+  if (a.skip && *a.skip) return;
+
+  for (int q = 0; q < NCK; ++q) {
+    const int off = a.tab[2 * q], sz = a.tab[2 * q + 1];
+    const cu32x4* src = reinterpret_cast<const cu32x4*>(a.img) + off;
+    for (int i = threadIdx.x; i < sz; i += NT) wl[q][i] = src[i];
+  }
+  for (int i = threadIdx.x; i < 3 * 64; i += NT) {
+    const int l = i >> 6, j = i & 63;
+    sbias[l][j] = j < a.w[l + 1] ? a.theta[a.offb[l] + j] : 0.0f;
+  }
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, s = lane & 15;
+  const int eX = __builtin_amdgcn_readfirstlane(amax_exp(a.am_x));
+  const int eH = f16_scale_exp(1.0f);
+  const int e0 = __builtin_amdgcn_readfirstlane(a.img_e[0]), e1 = __builtin_amdgcn_readfirstlane(a.img_e[1]);
+  const int e2 = __builtin_amdgcn_readfirstlane(a.img_e[2]);
+  const float sX = __builtin_ldexpf(1.0f, eX), sH = __builtin_ldexpf(1.0f, eH);
+  const float u0 = __builtin_ldexpf(1.0f, -(e0 + eX)), u1 = __builtin_ldexpf(1.0f, -(e1 + eH));
+  const float u2 = __builtin_ldexpf(1.0f, -(e2 + eH));
+  const int A = a.w[3], ld0 = a.ld[0], ldo = a.ld[3];
+  const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+
+  // acc[0, OT) += chunk (weights in LDS) x b
+  // the fragment offset is re-derived per group from an opaque copy: the weight fragments are the same for every
+  // group, and hoisted out of the loop they took 200+ registers
+  int frag = 0;
+  auto mma_chunk = [&](int q, auto OT_, const fh8 (&b)[2], f32x4 (&ac)[OTM]) __attribute__((always_inline)) {
+    constexpr int OT = decltype(OT_)::value, pl = OT * 512;
+    const unsigned short* W = reinterpret_cast<const unsigned short*>(&wl[q][0]) + frag;
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      fh8 f[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const fh8*>(W + p * pl + ot * 512);
+      ac[ot] = mfma3(f, b, ac[ot]);
+    }
+  };
+  // X tiles of a 16-state group (rows past n read 0)
+  f32x4 xb[KX][2];
+  auto load_x = [&](int64_t row_b) {
+    const int rb = (int)(row_b < a.n ? min<int64_t>(16, a.n - row_b) : 0);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.X + (row_b < a.n ? row_b : 0) * ld0), 0, rb * ld0 * 4, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < KX; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int col = 16 * (2 * c + h) + 4 * g;
+        const int vo = col < ld0 ? (s * ld0 + col) * 4 : rb * ld0 * 4;
+        xb[c][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
+      }
+  };
+  using C4 = std::integral_constant<int, OTM>;
+  using COTA = std::integral_constant<int, OTA>;
+
+  const int64_t ngroups = (a.n + 15) / 16, stride = (int64_t)gridDim.x * NW;
+  int64_t grp = (int64_t)blockIdx.x * NW + wave;
+  if (grp < ngroups) load_x(grp * 16);
+  for (; grp < ngroups; grp += stride) {
+    {
+      int t = threadIdx.x;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t));
+      const int ss = t & 15, gg = (t >> 4) & 3;
+      frag = ss * 32 + ((gg ^ chain_hsw(ss)) << 3);
+    }
+    f32x4 acc[OTM], H[OTM];
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) acc[t] = z4;
+#pragma unroll
+    for (int c = 0; c < KX; ++c) {
+      fh8 b[2];
+      mkb16(xb[c][0], xb[c][1], sX, b);
+      mma_chunk(c, C4{}, b, acc);
+    }
+    if (grp + stride < ngroups) load_x((grp + stride) * 16);   // the next group's X behind this group's math
+    // H_1 = tanh(X W_0 + b_0); padding features: zero weights and bias, tanh(0) = 0
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[0][16 * t + 4 * g]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u0, bb[i]));
+      acc[t] = z4;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      fh8 b[2];
+      mkb16(H[2 * c], H[2 * c + 1], sH, b);
+      mma_chunk(KX + c, C4{}, b, acc);
+    }
+#pragma unroll
+    for (int t = 0; t < OTM; ++t) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[1][16 * t + 4 * g]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u1, bb[i]));
+      acc[t] = z4;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      fh8 b[2];
+      mkb16(H[2 * c], H[2 * c + 1], sH, b);
+      mma_chunk(KX + 2 + c, COTA{}, b, acc);
+    }
+
+    // ---- softmax and the row terms (rowepi.h kLossHead): lane g holds actions 16t + 4g + i ----
+    const int64_t row = grp * 16 + s;
+    const bool rowvalid = row < a.n;
+    const int64_t rc = rowvalid ? row : a.n - 1;
+    const int av = a.act[rc];
+    const float advv = a.adv[rc];
+    constexpr int NA = 4 * OTA;
+    float z[NA], oldv[NA];
+    float zm = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < OTA; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = 16 * t + 4 * g + i;
+        const bool real = col < A;
+        z[4 * t + i] = real ? __builtin_fmaf(acc[t][i], u2, sbias[2][col]) : -INFINITY;
+        oldv[4 * t + i] = a.old[rc * ldo + (real ? col : 0)];
+        zm = fmaxf(zm, z[4 * t + i]);
+      }
+    const float m = xmax_f<false>(xmax_f<true>(zm));
+    float ex[NA], es = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      ex[k] = z[k] == -INFINITY ? 0.0f : expf(z[k] - m);
+      es += ex[k];
+    }
+    const float ssum = xadd_f<false>(xadd_f<true>(es));
+    float pa_l = 0.0f, olda_l = 0.0f, klp = 0.0f, enp = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OTA; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * t + i, col = 16 * t + 4 * g + i;
+        const bool real = col < A;
+        const float p = ex[k] / ssum;
+        const float old = (rowvalid && real) ? oldv[k] : 0.0f;
+        if (col == av) {
+          pa_l = p;
+          olda_l = old;
+        }
+        const float lk = logf((old + kEps) / (p + kEps)), le = logf(p + kEps);
+        klp += real ? old * lk : 0.0f;
+        enp += real ? -p * le : 0.0f;
+      }
+    const float pa = xadd_f<false>(xadd_f<true>(pa_l)), olda = xadd_f<false>(xadd_f<true>(olda_l));
+    const float klt = xadd_f<false>(xadd_f<true>(klp)), ent = xadd_f<false>(xadd_f<true>(enp));
+    if (rowvalid && g == 0) {
+      const double adv = advv;
+      a.rowterms[4 * row + 0] = (double)pa / (double)olda * adv;
+      a.rowterms[4 * row + 1] = klt;
+      a.rowterms[4 * row + 2] = ent;
+      a.rowterms[4 * row + 3] = 0.0;
+    }
+  }
+}
+
 int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
 
 template <int TI0, int MODE>
@@ -923,6 +1105,26 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
     if (j.which == which) maxb = std::max(maxb, (j.kc * j.otp * 4 + 255) / 256);
   }
   hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
+}
+
+void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {
+  if (a.n <= 0) return;
+  if (!fused16_eligible(3, a.w)) throw std::runtime_error("fwd_loss16: unsupported shape");
+  const int ti0 = ti0_of(a.w[0]);
+  if (a.nchunks != (ti0 + 1) / 2 + 4) throw std::runtime_error("fwd_loss16: chunk table");
+  const int64_t waves = (a.n + 15) / 16;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((waves + FWDL16_NW - 1) / FWDL16_NW, (int64_t)num_cus * 2));
+  const bool two = a.w[3] > 16;
+#define FWD_LOSS16(T)                                                                                             \
+  if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);            \
+  else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);
+  switch (ti0) {
+    case 1: FWD_LOSS16(1) break;
+    case 2: FWD_LOSS16(2) break;
+    case 4: FWD_LOSS16(4) break;
+    default: FWD_LOSS16(8) break;
+  }
+#undef FWD_LOSS16
 }
 
 void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<0>(a, grid, s); }

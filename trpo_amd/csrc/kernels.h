@@ -39,6 +39,8 @@ struct Options {
                    // 2 line search, and the prepare head when the head has <= 8 actions
   int splits;      // engine: weight-gradient split-K slabs of the FVP launches (0 = auto: 512 at C4)
   int pg_splits;   // engine: the policy gradient's split-K slabs (0 = auto: 4 x splits, at most 2048)
+  int ls_fused;    // engine: the line-search loss forward in one launch (fused16.hip fwd_loss16) where the FVP
+                   // runs on fused16: 0 off (per-layer row GEMMs + head_fwd), 1 (default) on
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -414,6 +416,27 @@ void launch_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
 // ... and with it, on the same weight chunks, the prepare pass's backward below the head: D_1, E_1, E_0 and D_1's
 // running max (engine.cpp prepare())
 void launch_prep_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
+// Line-search loss forward for the same shapes (fused16.hip fwd_loss16_kernel): the row terms of
+// trpo_inksci.py:46-53 at a trial theta, from that theta's W_0 | W_1 | W_2 images (ChainImgJob, which = 0, the
+// order here; img_e per job) resident in LDS, one wave per 16 states, no barrier in the loop.
+struct FwdLoss16Args {
+  int64_t n;
+  int w[4], ld[4];                   // widths [obs, h1, h2, A]; row strides
+  const float* X;
+  const float* theta;                // the trial vector (biases)
+  int64_t offb[3];
+  const void* img;                   // W_0 | W_1 | W_2 images (16-B units)
+  const int* tab;                    // per chunk (offset, size) in 16-B units
+  int nchunks;
+  const int* img_e;                  // [3]
+  const unsigned* am_x;
+  const float* old;                  // [n][ld[3]]
+  const int* act;
+  const float* adv;
+  double* rowterms;                  // [n][4]
+  const int* skip;
+};
+void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s);
 }  // namespace trpo
 
 namespace trpo {
