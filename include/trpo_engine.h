@@ -218,8 +218,9 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * prepare head when the head has <= 8 actions; 0 = off), "splits" (split-K slabs of the FVP's weight
  * gradients; 0 = auto: by tile count, at least one per 16k rows; 512 at C4, 245 at C5) and "pg_splits" (the
  * policy gradient's; 0 = auto: 4 x splits or one per 4k rows, up to 2048): both are read when an engine
- * is created; "ls_fused" (1 = where the FVP runs on fused16.hip, the line search's loss forward is one
- * launch from the trial vector's f16 weight images, fwd_loss16; the default; 0 = the per-layer forward).
+ * is created; "ls_fused" (where the FVP runs on fused16.hip, the policy forward as one launch from f16 weight
+ * images, fwd_loss16: 1 = the prepare pass's and the line search's, the default; 2 = the line search's only;
+ * 0 = the per-layer forwards).
  * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed
  * from the build in round 4; tools/patches/pruned_variants.patch restores them.
  * Process-wide. */

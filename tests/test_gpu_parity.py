@@ -348,9 +348,9 @@ def test_kernel_variants_parity(gpu_available, opts):
     (64, [64, 64], 16, 40_000),        # two obs chunks, one action tile exactly full
 ])
 def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
-    """The line-search loss forward in one launch (fused16.hip fwd_loss16, ls_fused = 1) at a trial theta against
-    the float64 oracle and the per-layer forward (ls_fused = 0): surr / kl / ent of trpo_inksci.py:46-53 through
-    loss() (:127-129)."""
+    """The policy forward in one launch (fused16.hip fwd_loss16, ls_fused = 1) against the float64 oracle and the
+    per-layer forward (ls_fused = 0): surr / kl / ent of trpo_inksci.py:46-53 at a trial theta through loss()
+    (:127-129, the line search), and at theta through the prepare pass (its softmax P and loss_before)."""
     from trpo_amd import Engine
     from trpo_amd._lib import get_option, set_option
     spec = O.PolicySpec(obs, hidden, A)
@@ -366,11 +366,20 @@ def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
             e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
             e.set_flat(dd["theta"])
             e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            out[(mode, "p")] = e.action_dist().astype(np.float64)
+            out[(mode, "lb")] = e.losses().astype(np.float64)
             out[mode] = e.eval_losses(trial).astype(np.float64)
             out[(mode, "again")] = e.eval_losses(trial).astype(np.float64)
             e.close()
     finally:
         set_option("ls_fused", saved)
+    _, p_ref = O.forward(dd["theta"].astype(np.float64), dd["X"], spec)
+    lb_ref = O.losses(dd["theta"].astype(np.float64), dd["X"], dd["actions"], dd["advant"], dd["old_dist"], spec)
+    for mode in (1, 0):
+        assert np.max(np.abs(out[(mode, "p")] - p_ref)) <= 1e-6, mode
+        assert out[(mode, "lb")][0] == pytest.approx(lb_ref[0], rel=REL, abs=1e-7), (mode, out[(mode, "lb")], lb_ref)
+        assert out[(mode, "lb")][1] == pytest.approx(lb_ref[1], rel=REL, abs=1e-7), (mode, out[(mode, "lb")], lb_ref)
+        assert out[(mode, "lb")][2] == pytest.approx(lb_ref[2], rel=REL), (mode, out[(mode, "lb")], lb_ref)
     for mode in (1, 0):
         got = out[mode]
         assert got[0] == pytest.approx(ref[0], rel=REL, abs=1e-7), (mode, got, ref)

@@ -1006,7 +1006,8 @@ struct trpo_engine {
     ensure_w3();
     am_reset(am_d(0), L);
     am_reset(am_ds(L - 1), 1);
-    forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
+    if (use_fused16() && g_options.ls_fused == 1) fused16_forward(theta, true);   // fwd_loss16's prepare form
+    else forward(WF, WF3, theta, H, RowEpi::kPrepHead, "fwd");
     // KL_ff plain backward: DH_l = D_l W_l^T ; D_{l-1} = DH (1-H^2) ; E_{l-1} = -2 DH H.
     // Only what the FVP path will read is written (prep_e_top records it; fvp() re-prepares if the
     // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
@@ -1599,38 +1600,51 @@ struct trpo_engine {
   }
 
   // loss(th) at a device parameter vector, without touching the prepared cache
+  // the policy forward in one launch from th's f16 weight images (fused16.hip fwd_loss16_kernel): the line search's
+  // row loss terms, or (prep) the prepare pass's H_1, H_2, P, D_2, DS_2, their maxima and the row terms
+  void fused16_forward(const float* th, bool prep) {
+    {
+      Scope sp(this, prep ? "fwd_img" : "ls_img");
+      launch_fused16_img(f16_ljobs, th, nullptr, 0, nullptr, f16_le, stream);
+      check_launch();
+    }
+    FwdLoss16Args la{};
+    la.n = n;
+    for (int l = 0; l <= L; ++l) {
+      la.w[l] = w[l];
+      la.ld[l] = wp[l];
+    }
+    la.X = X;
+    la.theta = th;
+    for (int l = 0; l < L; ++l) la.offb[l] = offb[l];
+    la.img = f16_limg;
+    la.tab = f16_ltab;
+    la.nchunks = f16_lnchunks;
+    la.img_e = f16_le;
+    la.am_x = am_x();
+    la.old = old;
+    la.act = act;
+    la.adv = adv32;
+    la.rowterms = rowterms;
+    if (prep) {
+      la.H1 = H[1];
+      la.H2 = H[2];
+      la.P = Pm;
+      la.D = D[L - 1];
+      la.DS = DSL;
+      la.am_d = am_d(L - 1);
+      la.am_ds = am_ds(L - 1);
+      la.invN = 1.0 / (double)n_global;
+    }
+    Scope sp(this, prep ? "fwd" : "ls_fwd");
+    launch_fwd_loss16(la, num_cus, stream);
+    check_launch();
+  }
+
   void eval_losses_dev(const float* th) {
     require_batch();
     if (use_fused16() && g_options.ls_fused != 0) {
-      // one launch from the trial vector's f16 images (fused16.hip fwd_loss16_kernel)
-      {
-        Scope sp(this, "ls_img");
-        launch_fused16_img(f16_ljobs, th, nullptr, 0, nullptr, f16_le, stream);
-        check_launch();
-      }
-      FwdLoss16Args la{};
-      la.n = n;
-      for (int l = 0; l <= L; ++l) {
-        la.w[l] = w[l];
-        la.ld[l] = wp[l];
-      }
-      la.X = X;
-      la.theta = th;
-      for (int l = 0; l < L; ++l) la.offb[l] = offb[l];
-      la.img = f16_limg;
-      la.tab = f16_ltab;
-      la.nchunks = f16_lnchunks;
-      la.img_e = f16_le;
-      la.am_x = am_x();
-      la.old = old;
-      la.act = act;
-      la.adv = adv32;
-      la.rowterms = rowterms;
-      {
-        Scope sp(this, "ls_fwd");
-        launch_fwd_loss16(la, num_cus, stream);
-        check_launch();
-      }
+      fused16_forward(th, false);
       reduce_losses(1, nullptr);
       return;
     }

@@ -883,11 +883,13 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 // of V), with the next group's X in flight behind the current group's math.  Products as the FVP: scaled f16
 // hi + lo, 3 products; H's scale fixed, X's from its running max, each weight image's from its builder.
 // The head: f32 softmax and logs, as the row GEMM's kLossHead (rowepi.h), over the state's 4 lanes.
+// PREP: the prepare pass's forward at theta instead (kPrepHead): H_1, H_2, P, the KL_ff logit delta D_2 and the
+// surr logit delta DS_2 stored, with D_2's and DS_2's running maxima, and the same row terms (loss_before).
 // ---------------------------------------------------------------------------------------------------------
 #ifndef FWDL16_NW
-#define FWDL16_NW 4   // waves per workgroup (sharing one LDS copy of the weights)
+#define FWDL16_NW 8   // waves per workgroup (sharing one LDS copy of the weights): C3 0.217 ms at 4, 0.201 at 8
 #endif
-template <int TI0, int OTA>
+template <int TI0, int OTA, bool PREP>
 __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const FwdLoss16Args a) {
   constexpr int OTM = 4, KX = (TI0 + 1) / 2, NW = FWDL16_NW, NT = 64 * NW;
   constexpr int NCK = KX + 4;                  // W_0 (KX chunks), W_1 (2), W_2 (2)
@@ -954,6 +956,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
 
   const int64_t ngroups = (a.n + 15) / 16, stride = (int64_t)gridDim.x * NW;
   int64_t grp = (int64_t)blockIdx.x * NW + wave;
+  float md = 0.0f, mds = 0.0f;   // PREP: running max |D_2|, |DS_2| of this lane
   if (grp < ngroups) load_x(grp * 16);
   for (; grp < ngroups; grp += stride) {
     {
@@ -972,6 +975,18 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       mma_chunk(c, C4{}, b, acc);
     }
     if (grp + stride < ngroups) load_x((grp + stride) * 16);   // the next group's X behind this group's math
+    // acc-layout tiles of this lane's state row -> a [n][ld] output (rows past n and columns past ld dropped)
+    const int64_t row_b = grp * 16;
+    const int rb = (int)min<int64_t>(16, a.n - row_b);
+    auto st_tiles = [&](float* out, int ld, int nt, const f32x4* x) {
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(out + row_b * ld), 0, rb * ld * 4, 0x00020000);
+      for (int t = 0; t < nt; ++t) {
+        const int col = 16 * t + 4 * g;
+        const int vo = col < ld ? (s * ld + col) * 4 : rb * ld * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(cu32x4, x[t]), r, vo, 0, 0);
+      }
+    };
     // H_1 = tanh(X W_0 + b_0); padding features: zero weights and bias, tanh(0) = 0
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
@@ -980,6 +995,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u0, bb[i]));
       acc[t] = z4;
     }
+    if constexpr (PREP) st_tiles(a.H1, a.ld[1], OTM, H);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       fh8 b[2];
@@ -993,6 +1009,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u1, bb[i]));
       acc[t] = z4;
     }
+    if constexpr (PREP) st_tiles(a.H2, a.ld[2], OTM, H);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       fh8 b[2];
@@ -1046,6 +1063,44 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       }
     const float pa = xadd_f<false>(xadd_f<true>(pa_l)), olda = xadd_f<false>(xadd_f<true>(olda_l));
     const float klt = xadd_f<false>(xadd_f<true>(klp)), ent = xadd_f<false>(xadd_f<true>(enp));
+    if constexpr (PREP) {
+      // KL_ff plain logit delta d_j = (p_j/N)(B_j - sum_k p_k B_k), B = eps/(p+eps), and the surr logit delta
+      // -(adv/(N old_a)) p_a (1[j=a] - p_j) (rowepi.h kPrepHead, f32)
+      const float invN = (float)a.invN;
+      float pv[NA], B[NA], spBp = 0.0f, restp = 0.0f;
+#pragma unroll
+      for (int t = 0; t < OTA; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * t + i, col = 16 * t + 4 * g + i;
+          const bool real = col < A;
+          pv[k] = real ? ex[k] / ssum : 0.0f;
+          B[k] = real ? kEps * __builtin_amdgcn_rcpf(pv[k] + kEps) : 0.0f;
+          spBp += pv[k] * B[k];
+          restp += (real && col != av) ? pv[k] : 0.0f;
+        }
+      const float spB = xadd_f<false>(xadd_f<true>(spBp)), rest = xadd_f<false>(xadd_f<true>(restp));
+      const float adv = rowvalid ? advv : 0.0f;
+      const float coef = -adv * invN / olda * pa;
+      f32x4 P4[OTA], D4[OTA], S4[OTA];
+#pragma unroll
+      for (int t = 0; t < OTA; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * t + i, col = 16 * t + 4 * g + i;
+          const bool real = col < A;
+          P4[t][i] = pv[k];
+          D4[t][i] = real ? pv[k] * invN * (B[k] - spB) : 0.0f;
+          S4[t][i] = real ? coef * (col == av ? rest : -pv[k]) : 0.0f;
+          if (rowvalid) {
+            md = fmaxf(md, fabsf(D4[t][i]));
+            mds = fmaxf(mds, fabsf(S4[t][i]));
+          }
+        }
+      st_tiles(a.P, ldo, OTA, P4);
+      st_tiles(a.D, ldo, OTA, D4);
+      st_tiles(a.DS, ldo, OTA, S4);
+    }
     if (rowvalid && g == 0) {
       const double adv = advv;
       a.rowterms[4 * row + 0] = (double)pa / (double)olda * adv;
@@ -1054,6 +1109,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       a.rowterms[4 * row + 3] = 0.0;
     }
   }
+  if constexpr (PREP) amax_commit3(a.am_d, md, a.am_ds, mds, nullptr, 0.0f);
 }
 
 int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
@@ -1109,6 +1165,8 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
 
 void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {
   if (a.n <= 0) return;
+  const bool prep = a.H1 != nullptr;
+  if (prep && (!a.H2 || !a.P || !a.D || !a.DS)) throw std::runtime_error("fwd_loss16 prepare: missing output");
   if (!fused16_eligible(3, a.w)) throw std::runtime_error("fwd_loss16: unsupported shape");
   const int ti0 = ti0_of(a.w[0]);
   if (a.nchunks != (ti0 + 1) / 2 + 4) throw std::runtime_error("fwd_loss16: chunk table");
@@ -1116,8 +1174,13 @@ void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((waves + FWDL16_NW - 1) / FWDL16_NW, (int64_t)num_cus * 2));
   const bool two = a.w[3] > 16;
 #define FWD_LOSS16(T)                                                                                             \
-  if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);            \
-  else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);
+  if (prep) {                                                                                                     \
+    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, true>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);     \
+    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, true>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);         \
+  } else {                                                                                                        \
+    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, false>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);    \
+    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, false>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);        \
+  }
   switch (ti0) {
     case 1: FWD_LOSS16(1) break;
     case 2: FWD_LOSS16(2) break;

@@ -39,8 +39,9 @@ struct Options {
                    // 2 line search, and the prepare head when the head has <= 8 actions
   int splits;      // engine: weight-gradient split-K slabs of the FVP launches (0 = auto: 512 at C4)
   int pg_splits;   // engine: the policy gradient's split-K slabs (0 = auto: 4 x splits, at most 2048)
-  int ls_fused;    // engine: the line-search loss forward in one launch (fused16.hip fwd_loss16) where the FVP
-                   // runs on fused16: 0 off (per-layer row GEMMs + head_fwd), 1 (default) on
+  int ls_fused;    // engine: the policy forwards in one launch (fused16.hip fwd_loss16) where the FVP runs on
+                   // fused16: 1 (default) the prepare pass's and the line search's, 2 the line search's only,
+                   // 0 neither (per-layer row GEMMs + head_fwd)
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -435,6 +436,15 @@ struct FwdLoss16Args {
   const float* adv;
   double* rowterms;                  // [n][4]
   const int* skip;
+  // the prepare pass (H1 != NULL): H_1, H_2 [n][ld[1|2]], P / D_2 / DS_2 [n][ld[3]] and the maxima of D_2, DS_2
+  float* H1 = nullptr;
+  float* H2 = nullptr;
+  float* P = nullptr;
+  float* D = nullptr;
+  float* DS = nullptr;
+  unsigned* am_d = nullptr;
+  unsigned* am_ds = nullptr;
+  double invN = 0.0;
 };
 void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s);
 }  // namespace trpo
