@@ -170,3 +170,13 @@ def test_fused_fvp_roofline_follows_the_issued_arithmetic():
     assert bench.tag_flops("pg_fused", c3, n) == 2.0 * n * ((64 * 64 + 64 * 18) + (128 * 64 + 64 * 64 + 64 * 18))
     assert bench.tag_bytes("pg_fused", c3, n) == 4.0 * n * sum(c3)
     assert bench.tag_is_split("pg_fused", c3) and bench.tag_products("pg_fused", c3) == 3
+    # fwd_loss16 (one-launch policy forwards): the whole forward's FLOPs; X + pi_old for the line search, plus
+    # H_1, H_2, P, D_2, DS_2 out for the prepare pass; per-layer tags keep their own pricing
+    fwd_flops = 2.0 * n * (128 * 64 + 64 * 64 + 64 * 18)
+    for tag in ("fwd", "ls_fwd"):
+        assert bench.tag_flops(tag, c3, n) == fwd_flops
+        assert bench.tag_is_split(tag, c3) and bench.tag_products(tag, c3) == 3
+        assert bench.tag_x_bytes(tag, c3, n) == 4.0 * n * 128
+    assert bench.tag_bytes("ls_fwd", c3, n) == 4.0 * n * (128 + 18)
+    assert bench.tag_bytes("fwd", c3, n) == 4.0 * n * (128 + 4 * 18 + 64 + 64)
+    assert bench.tag_flops("ls_fwd_l1", c3, n) == 2.0 * n * 64 * 64
