@@ -35,7 +35,8 @@
 #define FUSED16_LB 2   // workgroups per CU the register budget is sized for
 #endif
 // Ablation builds for profiling only (tools/variant.sh; never the shipped library): bit 0 = no per-state
-// activation loads, 1 = no gradient passes, 2 = no weight-chunk loads, 3 = no chunk barriers
+// activation loads, 1 = no gradient passes, 2 = no weight-chunk loads, 3 = no chunk barriers, 4 = no weight-chunk
+// loads with the chunks' LDS stores kept
 #ifndef FUSED16_ABL
 #define FUSED16_ABL 0
 #endif
@@ -247,6 +248,15 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   cu32x4 wr[WS][NLD];
   auto gload = [&](int set, int qq) {
     if constexpr ((FUSED16_ABL & 4) != 0) return;
+    if constexpr ((FUSED16_ABL & 16) != 0) {   // no weight loads, but the chunk's LDS stores kept (opaque values)
+#pragma unroll
+      for (int i = 0; i < NLD; ++i) {
+        unsigned u = qq + i;
+        asm volatile("" : "+v"(u));
+        wr[set][i] = cu32x4{u, u, u, u};
+      }
+      return;
+    }
     const int off = __builtin_amdgcn_readfirstlane(a.tab[2 * qq]);
     const int sz = __builtin_amdgcn_readfirstlane(a.tab[2 * qq + 1]);
 #pragma unroll
