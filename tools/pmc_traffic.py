@@ -27,6 +27,8 @@ SPECS = {
     "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 11, 2, 1, 2, 32>", 1, 0),  # kRZ into the tail (BK 32)
     "fvp_rbwdwg_l1": ("rbwd0_kernel<2>", 1, 0),                             # R-backward + X^T RD_0 (rbwd0.hip)
     "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
+    # C2 / C3: the one-launch FVP (fused16.hip mode 0; every substring must be in the name)
+    "fvp_fused": (("fvp_fused16_kernel<", ", 0>("), 1, 0),
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
@@ -46,7 +48,8 @@ def load(path, counter):
 
 
 def pick(rows, sub, period=None, phase=None, longest=False):
-    sel = [r for r in rows if sub in r[1]]
+    subs = sub if isinstance(sub, tuple) else (sub,)
+    sel = [r for r in rows if all(x in r[1] for x in subs)]
     if longest and sel:
         # the FVP launches are the majority: keep those near the median duration (a single dispatch
         # slowed down under the counters must not become the reference)
@@ -80,7 +83,7 @@ def main():
             continue
         rd = 2 * 1024 * statistics.mean(r[2] for r in f)
         wr = 1024 * statistics.mean(r[2] for r in w)
-        res["tags"][tag] = {"kernel": sub, "launches": len(f), "read_bytes": rd, "write_bytes": wr,
+        res["tags"][tag] = {"kernel": "".join(sub) if isinstance(sub, tuple) else sub, "launches": len(f), "read_bytes": rd, "write_bytes": wr,
                             "traffic_bytes": rd + wr, "pmc_run_ms": statistics.mean(r[3] for r in f)}
     res["fvp_total_bytes"] = sum(v["traffic_bytes"] for v in res["tags"].values())
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
