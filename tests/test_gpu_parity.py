@@ -288,6 +288,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"head_fwd": 0}, {"head_fwd": 2}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
     {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
     {"ls_fused": 0},                                          # the line search's per-layer forward on fused16 shapes
+    {"cg_fuse_reduce": 0},                                    # the CG's separate slab reduction on fused16 shapes
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -296,7 +297,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
                                            "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
-                                           "splits", "pg_splits", "ls_fused")}
+                                           "splits", "pg_splits", "ls_fused", "cg_fuse_reduce")}
     try:
         for k, v in opts.items():
             set_option(k, v)

@@ -1209,14 +1209,17 @@ struct trpo_engine {
   }
 
   // Hv (undamped, all ranks) for device vector v -> out ; no-op when *skip
-  void fvp(const float* v, float* out, const int* skip) {
+  // defer (single rank, the one-launch FVP): the slab reduction is left to the caller (the CG iteration fuses it),
+  // *defer receives the slab count; 0 when this FVP reduced into out itself
+  void fvp(const float* v, float* out, const int* skip, int* defer = nullptr) {
+    if (defer) *defer = 0;
     // the path changed since prepare(): E_{L-2} needed but not written
     if (prepared && e_top_needed() && !prep_e_top) prepared = false;
     prepare();
     ds_ready = false;   // the FVP's R-backward writes RD (DS_{L-2}'s scratch)
     pg_ready = false;   // ... and every FVP path the slabs
     if (use_fused16()) {
-      fvp_fused16(v, out, skip);
+      fvp_fused16(v, out, skip, defer && !multi_rank() && cg_fused_reduce_ok(P) ? defer : nullptr);
       return;
     }
     if (use_fused()) {
@@ -1499,7 +1502,7 @@ struct trpo_engine {
   }
 
   // the whole Hv in one launch on the f16 split (fused16.hip) + the slab reduction
-  void fvp_fused16(const float* v, float* out, const int* skip) {
+  void fvp_fused16(const float* v, float* out, const int* skip, int* defer = nullptr) {
     fused16_w_images();
     {
       Scope sp(this, "fvp_img_v");
@@ -1512,6 +1515,10 @@ struct trpo_engine {
       Scope sp(this, "fvp_fused");
       launch_fvp_fused16(fa, grid, stream);
       check_launch();
+    }
+    if (defer) {
+      *defer = grid;
+      return;
     }
     {
       Scope sp(this, "reduce");
@@ -1585,9 +1592,11 @@ struct trpo_engine {
     launch_cg_init(b, xo, r, p, P, partA, sc, fl, tol, damping, stream);
     check_launch();
     for (int it = 0; it < iters; ++it) {
-      fvp(p, hv, &fl->done[it]);
+      int slabs = 0;
+      fvp(p, hv, &fl->done[it], g_options.cg_fuse_reduce ? &slabs : nullptr);
       Scope sp(this, "cg_vec");
-      launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      if (slabs > 0) launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      else launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
       check_launch();
     }
   }
@@ -2690,6 +2699,7 @@ static int* option_slot(const std::string& k) {
   if (k == "splits") return &g_options.splits;
   if (k == "pg_splits") return &g_options.pg_splits;
   if (k == "ls_fused") return &g_options.ls_fused;
+  if (k == "cg_fuse_reduce") return &g_options.cg_fuse_reduce;
   throw ArgError("unknown option " + k);
 }
 

@@ -42,6 +42,8 @@ struct Options {
   int ls_fused;    // engine: the policy forwards in one launch (fused16.hip fwd_loss16) where the FVP runs on
                    // fused16: 1 (default) the prepare pass's and the line search's, 2 the line search's only,
                    // 0 neither (per-layer row GEMMs + head_fwd)
+  int cg_fuse_reduce;  // engine: single rank with the one-launch FVP: each CG iteration's slab reduction fused with
+                       // its z = Hv + damping p (vec.hip reduce_slab_kernel<true>): 1 (default) on, 0 off
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -255,6 +257,12 @@ void launch_cg_init(const float* b, float* x, float* r, float* p, int64_t n, dou
                     UpdScalars* sc, CGFlags* fl, float tol, float damping, hipStream_t s);
 void launch_cg_iter(const float* hv, float* x, float* r, float* p, float* z, int64_t n, UpdScalars* sc,
                     double* partials, double* partials2, CGFlags* fl, int it, hipStream_t s);
+// single rank, the one-launch FVP: its slab reduction fused with the iteration's z = Hv + damping p and p.z
+// (vec.hip), then the x / r and p updates; P up to kRedBlocks x 64 parameters
+bool cg_fused_reduce_ok(int64_t P);
+void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, float* x, float* r, float* p, float* z,
+                          int64_t n, UpdScalars* sc, double* partials, double* partials2, CGFlags* fl, int it,
+                          hipStream_t s);
 struct CGScalarsD {
   double rdotr[2];
   double alpha, mu;

@@ -14,6 +14,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdexcept>
+
 #pragma clang fp contract(off)
 
 namespace trpo {
@@ -61,9 +63,15 @@ __global__ void amax_kernel(const float* A, int64_t n, int w, int ld, unsigned* 
 // wave-load) and spreads the S slabs over 16 wave groups, each with 4 independent accumulators, so a
 // launch has P/64 x 1024 threads with several loads in flight each (one thread per parameter and a
 // serial S-long chain was latency-bound: 0.2 ms for 512 slabs).
+// PZ: the CG's next step fused in (single rank: Hv needs no all-reduce in between): z = Hv + damping p and the
+// block's p.z partial (cg_pz_kernel), partials past the last block zeroed so that cg_xr_kernel's fixed-length sum
+// holds
 constexpr int kRsCols = 64, kRsGroups = 16;
+template <bool PZ>
 __global__ void __launch_bounds__(kRsCols* kRsGroups)
-reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* out, const int* skip) {
+reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* out, const int* skip,
+                   const float* pv = nullptr, float* z = nullptr, const UpdScalars* sc = nullptr,
+                   double* partials = nullptr) {
   __shared__ float red[kRsGroups][kRsCols + 1];
   if (skip && *skip) return;
   const int c = threadIdx.x % kRsCols, g = threadIdx.x / kRsCols;
@@ -87,6 +95,21 @@ reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* o
 #pragma unroll
     for (int i = 0; i < kRsGroups; ++i) acc += red[i][c];
     out[p] = acc;
+  }
+  if constexpr (PZ) {
+    if (g == 0) {   // wave 0: the block's 64 parameters
+      double v = 0.0;
+      if (p < P) {
+        const float damp = sc->damping, pi = pv[p], hv = out[p];
+        const float zi = damp != 0.0f ? hv + damp * pi : hv;
+        z[p] = zi;
+        v = (double)pi * (double)zi;
+      }
+      v = wave_sum_d(v);
+      if (c == 0) partials[blockIdx.x] = v;
+    }
+    if (blockIdx.x == 0)
+      for (int i = (int)gridDim.x + threadIdx.x; i < kRedBlocks; i += blockDim.x) partials[i] = 0.0;
   }
 }
 
@@ -400,8 +423,23 @@ void launch_pack(const PackArgs& pa, const float* src, int which, const int* ski
 void launch_reduce_slab(const float* slab, int S, int64_t stride, int64_t P, float* out,
                         const int* skip, hipStream_t s) {
   if (P <= 0) return;
-  hipLaunchKernelGGL(reduce_slab_kernel, dim3((unsigned)((P + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups), 0, s,
-                     slab, S, stride, P, out, skip);
+  hipLaunchKernelGGL(reduce_slab_kernel<false>, dim3((unsigned)((P + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups), 0,
+                     s, slab, S, stride, P, out, skip, nullptr, nullptr, nullptr, nullptr);
+}
+
+bool cg_fused_reduce_ok(int64_t P) { return (P + kRsCols - 1) / kRsCols <= kRedBlocks; }
+
+void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, float* x, float* r, float* p, float* z,
+                          int64_t n, UpdScalars* sc, double* partials, double* partials2, CGFlags* fl, int it,
+                          hipStream_t s) {
+  if (!cg_fused_reduce_ok(n)) throw std::runtime_error("cg_iter_slabs: too many parameters for one partials row");
+  const int* skip = &fl->done[it];
+  hipLaunchKernelGGL(reduce_slab_kernel<true>, dim3((unsigned)((n + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups),
+                     0, s, slab, S, stride, n, hv, skip, p, z, sc, partials);
+  hipLaunchKernelGGL((cg_xr_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, x, r, p, z, n, sc,
+                     partials, partials2, it, skip);
+  hipLaunchKernelGGL((cg_p_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, r, p, n, sc,
+                     partials2, fl, it);
 }
 
 void launch_dot_partials(const float* a, const float* b, int64_t n, double* partials,
