@@ -148,8 +148,8 @@ def fused16_used(widths) -> bool:
     """Whether the one-launch FVP runs on the f16 split (engine.cpp use_fused16, fused16.hip fused16_eligible)."""
     from trpo_amd._lib import get_option
     w = widths
-    return (get_option("fused") == 3 and get_option("split_f16") != 0 and len(w) == 4 and 1 <= w[0] <= 128 and
-            48 < w[1] <= 64 and 48 < w[2] <= 64 and 1 <= w[3] <= 32)
+    return (get_option("fused") == 3 and get_option("split_f16") != 0 and len(w) in (3, 4) and 1 <= w[0] <= 128 and
+            all(1 <= h <= 64 for h in w[1:-1]) and 1 <= w[-1] <= 32)
 
 
 def tag_products(tag: str, widths) -> int:

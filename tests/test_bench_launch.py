@@ -156,8 +156,11 @@ def test_fused_fvp_roofline_follows_the_issued_arithmetic():
         set_option("fused", 3)
         assert bench.fused16_used(c3) and bench.tag_products("fvp_fused", c3) == 3
         assert bench.tag_peak("fvp_fused", c3) == pytest.approx(bench.PEAK_BF16_TFLOPS / 3)
-        assert not bench.fused16_used([4, 64, 2])              # one hidden layer: fused.hip
-        assert bench.tag_products("fvp_fused", [4, 64, 2]) == 6
+        assert bench.fused16_used([4, 64, 2])                  # one hidden layer (the reference policy): fused16
+        assert bench.tag_products("fvp_fused", [4, 64, 2]) == 3
+        assert bench.fused16_used([37, 50, 33, 7])             # hidden widths below 49: padded images
+        assert not bench.fused16_used([4, 65, 2])              # wider than 64: not a fused shape
+        assert not bench.fused16_used([4, 64, 64, 64, 2])      # three hidden layers
         set_option("fused", 2)
         assert bench.tag_products("fvp_fused", c3) == 6
         set_option("fused", 3)

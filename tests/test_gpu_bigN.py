@@ -187,8 +187,12 @@ def test_c4_8m_whole_update_vs_float64(gpu_available, updates_8m, truth_8m, vari
         ref, ref32 = t[f"f64_{key}"], t[f"f32_{key}"]
         floor = rel_l2(ref32, ref)
         bar = REL if variant == "default" else max(REL, 2.0 * floor)
-        print(f"{variant} {key}: rel L2 vs float64 {rel_l2(a[key], ref):.2e} (float32 reference {floor:.2e}, "
-              f"bar {bar:.1e})")
+        line = (f"C4 8M {variant} {key}: rel L2 vs float64 {rel_l2(a[key], ref):.2e} (float32 reference "
+                f"{floor:.2e}, bar {bar:.1e})")
+        print(line)
+        if os.environ.get("TRPO_MARGIN_LOG"):   # tools/gpu.sh keeps these margins in the evidence log
+            with open(os.environ["TRPO_MARGIN_LOG"], "a") as f:
+                f.write(line + "\n")
         assert_vec_close(a[key], ref, bar, f"{key}: {variant} vs float64 at 8M")
     for key in ("shs", "lm", "surr_after", "ent_after", "kl_after"):
         ref, ref32 = float(t[f"f64_{key}"]), float(t[f"f32_{key}"])

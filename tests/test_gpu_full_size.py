@@ -55,8 +55,12 @@ def test_full_size_update_vs_float64(full_run):
     assert sa["cg_iters"] == int(t["f64_cg_iters"]) == 10
     assert sa["k"] == int(t["f64_k"]) and bool(sa["reverted"]) == bool(t["f64_reverted"])
     for key in ("g", "stepdir", "fullstep", "theta"):
-        print(f"{cfg} {key}: rel L2 vs float64 {rel_l2(a[key], t[f'f64_{key}']):.2e} "
-              f"(float32 reference {rel_l2(t[f'f32_{key}'], t[f'f64_{key}']):.2e})")
+        line = (f"full size {cfg} {key}: rel L2 vs float64 {rel_l2(a[key], t[f'f64_{key}']):.2e} "
+                f"(float32 reference {rel_l2(t[f'f32_{key}'], t[f'f64_{key}']):.2e})")
+        print(line)
+        if os.environ.get("TRPO_MARGIN_LOG"):   # tools/gpu.sh keeps these margins in the evidence log
+            with open(os.environ["TRPO_MARGIN_LOG"], "a") as f:
+                f.write(line + "\n")
         assert_vec_close(a[key], t[f"f64_{key}"], REL, f"{key}: {cfg} vs float64 at full size")
     for key in ("shs", "lm", "surr_after", "ent_after"):
         assert sa[key] == pytest.approx(float(t[f"f64_{key}"]), rel=REL), key

@@ -1,0 +1,171 @@
+"""fused16.hip (the one-launch FVP on the scaled f16 hi + lo split, the default at C2 / C3 dims) in the regimes where
+its scaling can fail, against the float64 oracle and against the bf16x6 one-launch FVP (fused = 2).
+
+fused16 gives values made inside the launch a per-state exponent (chain-step B operands) and a per-64-state-group
+exponent (the gradient-pass images, whose k dimension runs over states); X, D_1, D_2 use running-max slots and H a
+fixed scale.  What stresses that:
+  * a saturated softmax (head weights x6 / x25): p_j at or below eps, the O(eps) KL_ff terms D / E comparable to the
+    R-terms (trpo_inksci.py:50,56-70: eps inside both logs);
+  * saturated tanh layers (X x20): 1 - H^2 as small as H's own f16 rounding (the first fused16 build was 12 % off
+    here);
+  * mixed magnitudes inside one 64-state group: a few states per group whose R-forward values are 2^15 larger than
+    their neighbours'.  `mixed`: the last few obs features get zero rows in W_0 and those states carry 2^15-sized
+    values there, so X W_0 is exact, H_1 stays unsaturated and RH_1 = (1 - H_1^2)(X V_0 + c_0) grows 2^15-fold;
+  * `mixed_illcond`: the same states scaled by 2^15 as whole rows (C2) or along the null space of W_0^T (C3).  Their
+    pre-activations X W_0 are then O(1) sums of 2^15-sized products, which float32 cannot form (2^15 x 2^-24 x
+    sqrt(obs) of cancellation error): every float32 evaluation misses float64 by ~1e-3 here, the reference's own
+    graph in float32 included (oracle dtype float32), and the engine's exact bf16x6 and row-GEMM paths alike
+    (tools/dbg_hard.py, profiles/r6b).  There the bar is the float32 graph's own error: fused16 must stay within
+    2x of it, block by block;
+  * partial and single-state groups.
+Each case: the undamped Hv per parameter block (each W_l / b_l against its own scale) and one whole update
+(stepdir, theta_new, the CG count and the line-search k) against the float64 oracle at 1e-5, and Hv against the
+fused = 2 path.  Margins go to $TRPO_MARGIN_LOG when it is set (tools/gpu.sh keeps them in the evidence log)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_vec_close, rel_l2
+from oracle import trpo_oracle as O
+
+pytestmark = pytest.mark.gpu
+REL = 1e-5
+
+DIMS = {"c2": (11, [64, 64], 3), "c3": (128, [64, 64], 18)}
+
+
+def log_margin(line):
+    path = os.environ.get("TRPO_MARGIN_LOG")
+    print(line)
+    if path:
+        with open(path, "a") as f:
+            f.write(line + "\n")
+
+
+def hard_batch(dims, regime, n, seed):
+    obs, hidden, A = DIMS[dims]
+    spec = O.PolicySpec(obs, hidden, A)
+    d = O.synthetic_batch(spec, n, seed=seed)
+    theta = d["theta"].astype(np.float64).copy()
+    X = d["X"].astype(np.float64).copy()
+    params = O.unflatten(theta, spec)
+    if regime.startswith("head"):
+        s = float(regime[4:])
+        params[-1][0][...] *= s
+        params[-1][1][...] *= s
+    elif regime == "tanh20":
+        X *= 20.0
+    elif regime == "mixed":
+        # W_0's last nz rows zero; a few states per group carry 2^15-sized values in those features only
+        nz = min(3, obs)
+        params[0][0][obs - nz:, :] = 0.0
+        rs = np.random.RandomState(seed + 1)
+        for g0 in range(0, n, 64):
+            for off in (3, 17, 40):
+                i = g0 + off
+                if i < n:
+                    X[i, obs - nz:] = 2.0 ** 15 * rs.standard_normal(nz)
+    elif regime.startswith("mixed_illcond"):
+        big_exp = int(regime[14:]) if regime.startswith("mixed_illcond:") else 15   # ":k": 2^k (diagnostics)
+        W0 = params[0][0]                                  # obs x h1
+        rs = np.random.RandomState(seed + 1)
+        if obs > W0.shape[1]:
+            # rows with X W_0 = 0: H_1 = tanh(b_0) unsaturated, RH_1 = (1 - H_1^2)(X V_0 + c_0) of order 2^15
+            q, _ = np.linalg.qr(W0, mode="complete")
+            null = q[:, W0.shape[1]:]
+            big = lambda: 2.0 ** big_exp * null @ rs.standard_normal(null.shape[1]) / np.sqrt(null.shape[1])
+        else:
+            big = None
+        for g0 in range(0, n, 64):
+            for off in (3, 17, 40):                        # a few states of every 64-state group
+                i = g0 + off
+                if i < n:
+                    X[i] = big() if big is not None else X[i] * 2.0 ** big_exp
+    else:
+        raise ValueError(regime)
+    theta = O.flatten(params)
+    X = X.astype(np.float32)
+    theta32 = theta.astype(np.float32)
+    old = O.action_dist(theta32.astype(np.float64), X, spec, np.float64)
+    # actions drawn from the policy, as a rollout would: a uniform draw hits p_old[a] = 0 under a saturated head,
+    # where the reference's un-eps'd ratio is inf (tests/test_gpu_degenerate.py)
+    u = np.random.RandomState(seed + 2).uniform(size=(n, 1))
+    actions = np.minimum((np.cumsum(old, axis=1) < u).sum(axis=1), A - 1)
+    old32 = old.astype(np.float32)
+    keep = old32[np.arange(n), actions] > 0
+    actions[~keep] = np.argmax(old32[~keep], axis=1)
+    return spec, dict(X=X, theta=theta32, actions=actions, advant=d["advant"], old_dist=old32)
+
+
+def run_engine(spec, b, fused, v, update):
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import VEC_STEPDIR, get_option, set_option
+    saved = get_option("fused")
+    try:
+        set_option("fused", fused)
+        n = b["X"].shape[0]
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=max(n, 16))
+        e.set_flat(b["theta"])
+        e.set_batch(b["X"], b["actions"], b["advant"].astype(np.float32), b["old_dist"])
+        out = {"hv": e.fvp(v, 0.0)}
+        if update:
+            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out.update(st=st, stepdir=e.get_vector(VEC_STEPDIR), theta=e.get_flat())
+        e.close()
+        return out
+    finally:
+        set_option("fused", saved)
+
+
+CASES = [(dims, regime, n) for dims in ("c2", "c3")
+         for regime in ("head6", "head25", "tanh20", "mixed", "mixed_illcond")
+         for n in ((3001,) if dims == "c2" else (2049,))]
+CASES += [("c3", "mixed", 65), ("c3", "head25", 1), ("c2", "tanh20", 1), ("c2", "mixed", 70)]
+
+
+@pytest.mark.parametrize("dims,regime,n", CASES, ids=[f"{d}-{r}-n{n}" for d, r, n in CASES])
+def test_fused16_hard_regimes(gpu_available, dims, regime, n):
+    from trpo_amd._lib import get_option
+    spec, b = hard_batch(dims, regime, n, seed=1000 + n)
+    th64 = b["theta"].astype(np.float64)
+    sat = float((b["old_dist"] < 1e-6).mean())
+    h1 = np.tanh(b["X"].astype(np.float64) @ O.unflatten(th64, spec)[0][0] + O.unflatten(th64, spec)[0][1])
+    tsat = float((1.0 - h1 ** 2 < 1e-6).mean())
+    v = np.random.RandomState(n + 9).standard_normal(spec.n_params).astype(np.float32)
+    ref = O.fvp_undamped(th64, b["X"], v.astype(np.float64), spec)
+    illcond = regime.startswith("mixed_illcond")
+    ref32 = O.fvp_undamped(b["theta"], b["X"], v, spec, dtype=np.float32) if illcond else None
+    assert get_option("fused") == 3
+    f16 = run_engine(spec, b, 3, v, update=n > 1 and not illcond)
+    bf6 = run_engine(spec, b, 2, v, update=False)
+    worst = 0.0
+    off = 0
+    for l, (Wl, bl) in enumerate(O.unflatten(ref.copy(), spec)):
+        for name, blk in (("W", Wl), ("b", bl)):
+            sz = blk.size
+            got, want = f16["hv"][off:off + sz], ref[off:off + sz]
+            worst = max(worst, rel_l2(got, want))
+            if illcond:   # beyond float32: within 2x of the float32 graph's own error (and of fused = 2's)
+                floor = max(rel_l2(ref32[off:off + sz], want), rel_l2(bf6["hv"][off:off + sz], want))
+                assert rel_l2(got, want) <= max(REL, 2.0 * floor), (name, l, rel_l2(got, want), floor)
+            else:
+                assert_vec_close(got, want, REL, f"{dims} {regime} Hv block {name}{l}")
+            off += sz
+    if not illcond:
+        assert_vec_close(f16["hv"], ref, REL, f"{dims} {regime} Hv")
+        assert_vec_close(f16["hv"], bf6["hv"], REL, f"{dims} {regime} fused16 vs fused=2 Hv")
+    line = (f"fused16 {dims} {regime} n={n}: p<1e-6 {sat:.2f}, 1-H1^2<1e-6 {tsat:.2f}; Hv rel L2 "
+            f"{rel_l2(f16['hv'], ref):.2e} (worst block {worst:.2e}; fused=2 {rel_l2(bf6['hv'], ref):.2e}"
+            + (f"; float32 graph {rel_l2(ref32, ref):.2e}" if illcond else "") + ")")
+    if n > 1 and not illcond:
+        r = O.trpo_update(th64, O.Batch(b["X"], b["actions"], b["advant"], b["old_dist"]), spec, np.float64, 10, 0.0)
+        st = f16["st"]
+        assert st["cg_iters"] == r.cg_iters == 10
+        assert st["k"] == r.k
+        assert bool(st["reverted"]) == bool(r.reverted)
+        assert_vec_close(f16["stepdir"], r.stepdir, REL, f"{dims} {regime} stepdir")
+        assert_vec_close(f16["theta"], r.theta_new, REL, f"{dims} {regime} theta_new")
+        line += (f"; stepdir {rel_l2(f16['stepdir'], r.stepdir):.2e}, theta_new {rel_l2(f16['theta'], r.theta_new):.2e}"
+                 f", k {st['k']}")
+    log_margin(line)

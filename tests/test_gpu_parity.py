@@ -288,6 +288,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"head_fwd": 0}, {"head_fwd": 2}, {"head_fwd": 0, "chain": 0},   # the f32 MFMA row GEMM's 32-lane softmax head
     {"splits": 64, "pg_splits": 256}, {"splits": 3000, "pg_splits": 100},   # other split-K geometries
     {"ls_fused": 0},                                          # the line search's per-layer forward on fused16 shapes
+    {"ls_fused": 2},                                          # per-layer prepare forward, one-launch trial forwards
     {"cg_fuse_reduce": 0},                                    # the CG's separate slab reduction on fused16 shapes
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
@@ -347,6 +348,10 @@ def test_kernel_variants_parity(gpu_available, opts):
     (40, [64, 49], 32, 777),           # 4 obs tiles, a partial hidden tile, two action tiles
     (20, [56, 64], 17, 1),             # one state
     (64, [64, 64], 16, 40_000),        # two obs chunks, one action tile exactly full
+    (4, [64], 2, 1000),                # C1 dims: one hidden layer (the reference policy, trpo_inksci.py:38-40)
+    (128, [32], 32, 4099),             # one hidden layer of 32 (padded to 64), two action tiles
+    (37, [50, 33], 7, 129),            # hidden widths below 49 (padded images)
+    (16, [17, 48], 17, 1),             # one state, narrow widths
 ])
 def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
     """The policy forward in one launch (fused16.hip fwd_loss16, ls_fused = 1) against the float64 oracle and the
@@ -394,6 +399,9 @@ def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
     (128, [64, 64], 18, 100_000),      # C3 dims, many groups per persistent workgroup
     (40, [64, 49], 32, 777),           # 4 obs tiles, a partial hidden tile, A = 32
     (20, [56, 64], 17, 1),             # one state
+    (4, [64], 2, 1000),                # C1 dims: one hidden layer
+    (128, [32], 32, 63),               # one hidden layer of 32, a single partial group
+    (37, [50, 33], 7, 129),            # hidden widths below 49
 ])
 def test_fused16_policy_grad_vs_oracle(gpu_available, obs, hidden, A, n):
     """The policy gradient in one launch (fused16.hip's PG form, fused = 3) against the float64 oracle and the
@@ -464,11 +472,13 @@ def test_chain_shapes_vs_oracle(gpu_available, obs, hidden, A, n):
     (128, [64, 64], 3, 4099),          # f16 form: 8 obs tiles, one head tile
     (40, [64, 49], 32, 777),           # f16 form: 4 obs tiles, a partial hidden tile, A = 32
     (20, [56, 64], 17, 300),           # f16 form: 2 obs tiles
+    (4, [64], 2, 100_000),             # C1 dims, many groups per persistent workgroup
+    (11, [17], 3, 3001),               # one hidden layer of 17 (padded to 64)
 ])
 def test_fused_fvp_vs_oracle(gpu_available, obs, hidden, A, n):
-    """The one-launch FVP (fused.hip, both workgroup forms; fused16.hip on the f16 split where it applies,
-    mode 3) against the float64 oracle and against the chain + weight-gradient GEMM path it replaces
-    (trpo_inksci.py:56-70)."""
+    """The one-launch FVP (fused.hip, both workgroup forms; fused16.hip on the f16 split, mode 3: every shape here,
+    one or two hidden layers of width <= 64) against the float64 oracle and against the chain + weight-gradient GEMM
+    path it replaces (trpo_inksci.py:56-70)."""
     from trpo_amd import Engine
     from trpo_amd._lib import get_option, set_option
     spec = O.PolicySpec(obs, hidden, A)
@@ -823,6 +833,36 @@ def test_path_switch_after_prepare_rewrites_e(gpu_available):
         e.close()
     finally:
         set_option("tail", saved)
+
+
+def test_fused16_switch_after_prepare(gpu_available):
+    """prepare() on the fused16 path writes D_1 / E_1 / E_0 and the policy gradient's slabs from one launch
+    (bwd_pg), not the per-layer path's outputs. Switching option fused on the same engine afterwards must
+    re-prepare (engine.cpp reprepare_if_path_changed), in both directions, for fvp() and policy_grad()."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(128, [64, 64], 18)
+    n = 3001
+    d = O.synthetic_batch(spec, n, seed=41)
+    v = np.random.RandomState(42).standard_normal(spec.n_params).astype(np.float32)
+    th = d["theta"].astype(np.float64)
+    ref = O.fvp_undamped(th, d["X"], v.astype(np.float64), spec)
+    gref = O.policy_grad(th, d["X"], d["actions"], d["advant"], d["old_dist"], spec)
+    saved = get_option("fused")
+    try:
+        set_option("fused", 3)
+        e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+        e.set_flat(d["theta"])
+        e.set_batch(d["X"], d["actions"], d["advant"].astype(np.float32), d["old_dist"])
+        assert_vec_close(e.policy_grad(), gref, REL, "g, fused16")
+        for mode in (2, 0, 3, 0):
+            set_option("fused", mode)
+            assert_vec_close(e.policy_grad(), gref, REL, f"g after switching to fused={mode}")
+            assert_vec_close(e.fvp(v, 0.0), ref, REL, f"Hv after switching to fused={mode}")
+            assert_vec_close(e.policy_grad(), gref, REL, f"g after an FVP on fused={mode}")
+        e.close()
+    finally:
+        set_option("fused", saved)
 
 
 def test_flatgrad_of_gvp_is_the_fvp(gpu_available):

@@ -33,7 +33,8 @@ print('%s %.4f upd/s  %.2f ms/update  %.3f ms/FVP  dominant %s %.3f ms frac %.3f
 case $CMD in
   tests)
     if [ -n "$1" ]; then K=(-k "$1"); else K=(); fi
-    timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+    TRPO_MARGIN_LOG=$OUT/margins.txt timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 \
+      --timeout-method thread "${K[@]}" \
       > $OUT/pytest_gpu.log 2>&1
     rc=$?; tail -3 $OUT/pytest_gpu.log; exit $rc ;;
   smoke)

@@ -162,6 +162,11 @@ struct trpo_engine {
   // but the fused tail, which recomputes it (tail.hip)
   bool e_top_needed() const { return L < 2 || !use_tail() || use_fused() || use_chain(); }
   bool prep_e_top = true;    // prepare() wrote E_{L-2}
+  bool prep_fused16 = false; // prepare() took the fused16 branch (D_1 / E_1 / E_0 and the pg slabs from bwd_pg)
+  // prepare()'s outputs belong to the other kernel path when option fused / split_f16 changed after it ran
+  void reprepare_if_path_changed() {
+    if (prepared && ((e_top_needed() && !prep_e_top) || prep_fused16 != use_fused16())) prepared = false;
+  }
 
   // fused FVP chain (chain.hip): weight images in consumption order + chunk table
   int chain_otm = 0;         // register tiles per hidden layer; 0 = shape not eligible
@@ -501,8 +506,9 @@ struct trpo_engine {
     chain_otm = otm;
   }
 
-  // fused16.hip's images: the chain's job order with 2 f16 planes per chunk and V_0 padded to
-  // fused16_obs_chunks(obs) chunks
+  // fused16.hip's images: the chain's job order with 2 f16 planes per chunk, V_0 padded to
+  // fused16_obs_chunks(obs) chunks and every hidden dimension to 64 (2 chunks of K, 64 rows of O: the kernel's
+  // hidden layers are 4 tiles of 16 whatever the width, the padding zeros)
   void setup_fused16() {
     if (!fused16_eligible(L, w.data())) return;
     std::vector<int> tab;
@@ -511,7 +517,9 @@ struct trpo_engine {
     ChainImgArgs* jobs = &f16_jobs;
     auto seg = [&](int l, int trans, int which) {
       const int K = trans ? w[l + 1] : w[l], O = trans ? w[l] : w[l + 1];
-      const int kc = l == 0 ? fused16_obs_chunks(w[0]) : (K + 31) / 32, otp = (O + 15) / 16 * 16, csz = otp * 8;
+      const bool k_hidden = trans ? l + 1 < L : l > 0, o_hidden = trans ? true : l + 1 < L;
+      const int kc = l == 0 && !trans ? fused16_obs_chunks(w[0]) : k_hidden ? 2 : (K + 31) / 32;
+      const int otp = o_hidden ? 64 : (O + 15) / 16 * 16, csz = otp * 8;
       ChainImgJob& j = jobs->job[nj++];
       j.src_off = offW[l];
       j.dst_off = off16 * 8;
@@ -538,7 +546,7 @@ struct trpo_engine {
       seg(l, 1, 0);
       seg(l, 1, 1);
     }
-    REQUIRE(nj == kFused16Jobs, "fused16: job count");
+    REQUIRE(nj == (L == 3 ? kFused16Jobs : 5), "fused16: job count");
     f16_jobs.n = nj;
     f16_img = dalloc<uint16_t>((size_t)off16 * 8);
     f16_tab = dalloc<int>(tab.size());
@@ -1013,6 +1021,7 @@ struct trpo_engine {
     // path changes): D_0 never (the R-backward stops at RD_0), E_{L-2} not under the fused tail, which
     // recomputes it from H and D_{L-1}.
     prep_e_top = e_top_needed();
+    prep_fused16 = use_fused16();
     ds_ready = false;
     pg_ready = false;
     d1_plane = false;
@@ -1022,10 +1031,10 @@ struct trpo_engine {
       // D_1, E_1, E_0 and the policy gradient's slabs in one launch on the f16 weight images (fused16.hip)
       fused16_w_images();
       Fused16Args fa = fused16_args(nullptr, nullptr, pg_grid);
-      fa.D1out = D[1];
-      fa.E1out = E[1];
+      fa.D1out = L == 3 ? D[1] : nullptr;   // one hidden layer: E_0 only (D_1 is the head's delta)
+      fa.E1out = L == 3 ? E[1] : nullptr;
       fa.E0out = E[0];
-      fa.am_d1_out = am_d(1);
+      fa.am_d1_out = L == 3 ? am_d(1) : nullptr;
       {
         Scope sp(this, "bwd_pg");
         launch_prep_pg_fused16(fa, pg_grid, stream);
@@ -1153,6 +1162,7 @@ struct trpo_engine {
 
   // flatgrad(surr) (trpo_inksci.py:54) -> g (all ranks)
   void policy_grad() {
+    reprepare_if_path_changed();
     prepare();
     if (use_fused16()) {
       if (!pg_ready) pg_fused16();
@@ -1213,8 +1223,8 @@ struct trpo_engine {
   // *defer receives the slab count; 0 when this FVP reduced into out itself
   void fvp(const float* v, float* out, const int* skip, int* defer = nullptr) {
     if (defer) *defer = 0;
-    // the path changed since prepare(): E_{L-2} needed but not written
-    if (prepared && e_top_needed() && !prep_e_top) prepared = false;
+    // the path changed since prepare(): E_{L-2} needed but not written, or the other side of the fused16 switch
+    reprepare_if_path_changed();
     prepare();
     ds_ready = false;   // the FVP's R-backward writes RD (DS_{L-2}'s scratch)
     pg_ready = false;   // ... and every FVP path the slabs
@@ -1484,7 +1494,7 @@ struct trpo_engine {
     fa.img_e = f16_e;
     fa.am_x = am_x();
     fa.am_d1 = am_d(1);
-    fa.am_d2 = am_d(2);
+    fa.am_d2 = L == 3 ? am_d(2) : nullptr;
     fa.DS = DSL;
     fa.am_ds2 = am_ds(L - 1);
     const int64_t slots = std::max<int64_t>(
@@ -1619,6 +1629,7 @@ struct trpo_engine {
     }
     FwdLoss16Args la{};
     la.n = n;
+    la.L = L;
     for (int l = 0; l <= L; ++l) {
       la.w[l] = w[l];
       la.ld[l] = wp[l];
@@ -1637,7 +1648,7 @@ struct trpo_engine {
     la.rowterms = rowterms;
     if (prep) {
       la.H1 = H[1];
-      la.H2 = H[2];
+      la.H2 = L == 3 ? H[2] : nullptr;
       la.P = Pm;
       la.D = D[L - 1];
       la.DS = DSL;
@@ -1787,8 +1798,8 @@ struct trpo_engine {
   GraphKey upd_key{};
   bool upd_key_seen = false, graphs_broken = false;
   struct PrefixFlags {
-    bool prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, ds_ready, pg_ready, d1_plane,
-        d1_tiled;
+    bool prepared, w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top, prep_fused16, ds_ready, pg_ready,
+        d1_plane, d1_tiled;
     int pg_grid;
   } upd_flags{};
   void drop_graph() {
@@ -1818,6 +1829,7 @@ struct trpo_engine {
       f16_w_valid = upd_flags.f16_w_valid;
       have_returns = upd_flags.have_returns;
       prep_e_top = upd_flags.prep_e_top;
+      prep_fused16 = upd_flags.prep_fused16;
       ds_ready = upd_flags.ds_ready;
       pg_ready = upd_flags.pg_ready;
       pg_grid = upd_flags.pg_grid;
@@ -1857,8 +1869,8 @@ struct trpo_engine {
       update_prefix(prm);
       return;
     }
-    upd_flags = PrefixFlags{prepared, w3_valid,   chain_w_valid, f16_w_valid, have_returns, prep_e_top,
-                            ds_ready, pg_ready, d1_plane,      d1_tiled,    pg_grid};
+    upd_flags = PrefixFlags{prepared,   w3_valid, chain_w_valid, f16_w_valid, have_returns, prep_e_top,
+                            prep_fused16, ds_ready, pg_ready,    d1_plane,    d1_tiled,     pg_grid};
     har_graph_end = har_next;   // the graph's host nodes own these slots from now on
     HIPCHECK(hipGraphLaunch(upd_exec, stream));
     if (har_graph_end) har_pending = true;

@@ -1,8 +1,10 @@
 // Fused small-width Fisher-vector product on the f16 split (gfx950 / CDNA4).
 //
 // The whole FVP of trpo_inksci.py:56-70 (Pearlmutter's R-operator) for a policy
-// with two tanh hidden layers of width 49..64, obs <= 128 and <= 32 actions (C2, C3) in one persistent
-// launch per shard, structured as fused.hip (16 states per wave through the R-forward, the R-softmax head
+// with one or two tanh hidden layers of width <= 64 (NH = 1: the reference's own [64] policy, trpo_inksci.py:38-40;
+// NH = 2: C2, C3), obs <= 128 and <= 32 actions in one persistent launch per shard.  Hidden widths below 64 run on
+// images padded to 64 features with zero weights (the image builder; padded features are tanh(0) = 0 with zero
+// tangents and deltas, so they add exact zeros), structured structured as fused.hip (16 states per wave through the R-forward, the R-softmax head
 // and the R-backward in MFMA accumulator layout; per-group weight-gradient passes over two LDS images;
 // one slab per workgroup) with three differences:
 //
@@ -168,15 +170,23 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
   *reinterpret_cast<cu32x4*>(dst + (size_t)j.otp * 32) = L;
 }
 
-// image jobs (kernels.h, kFused16Jobs)
+// image jobs (kernels.h, kFused16Jobs): NH = 2: V_0 | W_1 V_1 | W_2 V_2 | W_2^T V_2^T | W_1^T V_1^T;
+// NH = 1: V_0 | W_1 V_1 | W_1^T V_1^T
 enum { jV0 = 0, jW1, jV1, jW2, jV2, jW2t, jV2t, jW1t, jV1t };
+template <int NH> constexpr int fused16_jobs() { return NH == 2 ? 9 : 5; }
+template <int NH> constexpr int job_w1t() { return NH == 2 ? jW1t : 3; }
 
 // FW = waves per workgroup, TI0 = 16-feature tiles of obs (1, 2, 4, 8), OTA = 16-action tiles of the head;
 // MODE: 0 the FVP; 1 the policy gradient instead (the same machinery on the backward chain alone); 2 the policy
-// gradient and, on the same weight chunks, the prepare pass's backward below the head (D_1, E_1, E_0)
-template <int FW, int LB, int TI0, int OTA, int MODE>
+// gradient and, on the same weight chunks, the prepare pass's backward below the head (NH = 2: D_1, E_1, E_0;
+// NH = 1: E_0); NH = hidden layers (1 or 2)
+template <int FW, int LB, int TI0, int OTA, int MODE, int NH>
 __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16Args fa) {
   constexpr bool PG = MODE >= 1, PREP = MODE == 2;
+  static_assert(NH == 1 || NH == 2, "fused16: one or two hidden layers");
+  constexpr int LH = NH + 1;                   // index of the action width in w[] / ld[]
+  constexpr int NJ = fused16_jobs<NH>();
+  constexpr int JW1T = job_w1t<NH>();
   constexpr int OTM = 4;                       // 16-feature tiles of a hidden layer
   constexpr int NT = FW * 64;
   constexpr int CHU = 8 * 16 * OTM;            // 16-B units of a 64-row chunk: 2 planes x 64 rows x 64 B
@@ -207,7 +217,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   for (int i = threadIdx.x; i < FW * 3 * 64; i += NT) (&sb[0][0][0])[i] = 0.0f;
   for (int i = threadIdx.x; i < 3 * 64; i += NT) {   // (no tangent in the policy gradient)
     const int l = i >> 6, j = i & 63;
-    sc[l][j] = !PG && j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
+    sc[l][j] = !PG && l <= NH && j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
   }
 
   // scale exponents (wave-uniform)
@@ -216,9 +226,9 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   const int eD2 = __builtin_amdgcn_readfirstlane(amax_exp(fa.am_d2));
   const int eDS = PG ? __builtin_amdgcn_readfirstlane(amax_exp(fa.am_ds2)) : 0;
   const int eH = f16_scale_exp(1.0f);
-  int ej[kFused16Jobs];
+  int ej[NJ];
 #pragma unroll
-  for (int i = 0; i < kFused16Jobs; ++i) ej[i] = __builtin_amdgcn_readfirstlane(fa.img_e[i]);
+  for (int i = 0; i < NJ; ++i) ej[i] = __builtin_amdgcn_readfirstlane(fa.img_e[i]);
   const float sX = __builtin_ldexpf(1.0f, eX), sH = __builtin_ldexpf(1.0f, eH);
   const float sD1 = __builtin_ldexpf(1.0f, eD1), sD2 = __builtin_ldexpf(1.0f, eD2);
 
@@ -240,10 +250,10 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // weight chunks in flight WS ahead, in WS register sets: chunk c of a group sits in set c % WS (the group's
   // chunk count NCH need not be a multiple of WS: the next group's chunk k < WS is loaded into set k by whichever
   // of the last WS chunks frees that set)
-  constexpr int NCH = PG ? 3 : KX + 14;   // chunks per group
+  constexpr int NCH = PG ? (NH == 2 ? 3 : 1) : KX + (NH == 2 ? 14 : 6);   // chunks per group
   // image chunk (table index) of the group's chunk q: the FVP streams the whole image, the policy gradient
-  // W_2^T (one chunk) and W_1^T (two)
-  auto chunk_of = [&](int q) { return PG ? (q == 0 ? KX + 8 : KX + 9 + q) : q; };
+  // W_2^T (one chunk) and W_1^T (two); with one hidden layer W_1^T (one chunk: K = actions)
+  auto chunk_of = [&](int q) { return PG ? (NH == 1 ? KX + 4 : q == 0 ? KX + 8 : KX + 9 + q) : q; };
   constexpr int WS = FUSED16_WSETS;
   cu32x4 wr[WS][NLD];
   auto gload = [&](int set, int qq) {
@@ -509,37 +519,43 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     using C0 = std::integral_constant<int, 0>;
 
     if constexpr (PG) {
-      // ---- policy gradient (trpo_inksci.py:54): DS_1 = (DS_2 W_2^T)(1 - H_2^2),
-      //      DS_0 = (DS_1 W_1^T)(1 - H_1^2); g_W_l = H_l^T DS_l (H_0 = X), g_b_l = colsum DS_l.
-      //      DS_2 is the head's surr logit delta from the prepare pass. ----
+      // ---- policy gradient (trpo_inksci.py:54), the surr backward from the head's logit delta DS_h
+      //      (the prepare pass's): NH = 2: DS_1 = (DS_2 W_2^T)(1 - H_2^2), DS_0 = (DS_1 W_1^T)(1 - H_1^2);
+      //      NH = 1: DS_0 = (DS_1 W_1^T)(1 - H_1^2); g_W_l = H_l^T DS_l (H_0 = X), g_b_l = colsum DS_l. ----
       const float sDS = __builtin_ldexpf(1.0f, eDS);
-      // PREP: the KL_ff plain backward on the same chunks, DH_1 = D_2 W_2^T, D_1 = DH_1 (1 - H_2^2),
-      // E_1 = -2 DH_1 H_2, E_0 = -2 (D_1 W_1^T) H_1 (engine.cpp prepare(); D_0 has no reader)
+      // PREP: the KL_ff plain backward on the same chunks from the head's delta D_h:
+      //   NH = 2: DH_1 = D_2 W_2^T, D_1 = DH_1 (1 - H_2^2), E_1 = -2 DH_1 H_2, E_0 = -2 (D_1 W_1^T) H_1;
+      //   NH = 1: E_0 = -2 (D_1 W_1^T) H_1 (engine.cpp prepare(); D_0 has no reader)
+      const float sDh = NH == 2 ? sD2 : sD1;
+      const int eDh = NH == 2 ? eD2 : eD1;
       f32x4 accD[OTM], D1v[OTM];
       f32x4 d2c0 = z4, d2c1 = z4;
       if constexpr (PREP) {
-        const __amdgpu_buffer_rsrc_t rd2 = rsrc(a.D[2], a.ld[3]);
-        d2c0 = ld4(rd2, voff(a.ld[3], 0));
-        d2c1 = ld4(rd2, voff(a.ld[3], 1));
+        const __amdgpu_buffer_rsrc_t rd2 = rsrc(a.D[NH], a.ld[LH]);
+        d2c0 = ld4(rd2, voff(a.ld[LH], 0));
+        d2c1 = ld4(rd2, voff(a.ld[LH], 1));
 #pragma unroll
         for (int t = 0; t < OTM; ++t) accD[t] = z4;
       }
       auto extra1 = [&](int) {
         if constexpr (PREP) {
           fh8 b[2];
-          mkb16(d2c0, d2c1, sD2, b);
+          mkb16(d2c0, d2c1, sDh, b);
           mma_to(C4{}, b, accD);
         }
       };
-      step(C4{}, C0{}, C1{}, jW2t, 0, fa.DS, a.ld[3], sDS, eDS, a.H[2], a.ld[2], OTM, sD, false, extra1);
-      f32x4 DS1[OTM];
-      const float suD = __builtin_ldexpf(1.0f, -(ej[jW2t] + eD2));
+      // the head layer's backward step: its memory segment DS_h is captured into sD (the head pass's delta image)
+      step(C4{}, C0{}, C1{}, NH == 2 ? jW2t : JW1T, 0, fa.DS, a.ld[LH], sDS, eDS, a.H[NH], a.ld[NH], OTM, sD, false,
+           extra1);
+      const float suD = __builtin_ldexpf(1.0f, -(ej[NH == 2 ? jW2t : JW1T] + eDh));
+      f32x4 DS1[OTM];   // NH = 2: DS_1; NH = 1: DS_0 (also in S)
 #pragma unroll
       for (int t = 0; t < OTM; ++t) {
         const f32x4 h = PF[t];
+        if constexpr (NH == 1) H1f[t] = h;
 #pragma unroll
         for (int i = 0; i < 4; ++i) DS1[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));
-        put4(sA, t, h, sH);   // H_2, the head layer's pass operand (sA is free: past this step's chunk barrier)
+        put4(sA, t, h, sH);   // H_NH, the head layer's pass operand (sA is free: past this step's chunk barrier)
         if constexpr (PREP) {
           f32x4 e1;
 #pragma unroll
@@ -548,43 +564,53 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
             D1v[t][i] = dh * c_one_minus_sq(h[i]);
             e1[i] = -2.0f * dh * h[i];
           }
-          st4(fa.D1out, a.ld[2], t, D1v[t]);
-          st4(fa.E1out, a.ld[2], t, e1);
+          if constexpr (NH == 2) {
+            st4(fa.D1out, a.ld[2], t, D1v[t]);
+            st4(fa.E1out, a.ld[2], t, e1);
+          } else {
+            st4(fa.E0out, a.ld[1], t, e1);
+          }
         }
       }
-      float mst = state_max<OTM>(DS1);
-      wave_max(3, mst);
-      float mstD = 0.0f;
-      if constexpr (PREP) {
-        mstD = state_max<OTM>(D1v);
-        mD1 = fmaxf(mD1, mstD);
-#pragma unroll
-        for (int t = 0; t < OTM; ++t) accD[t] = z4;
-      }
-      const float sD1s = __builtin_ldexpf(1.0f, f16_scale_exp(mstD));
-      auto extra2 = [&](int c) {
+      if constexpr (NH == 2) {
+        float mst = state_max<OTM>(DS1);
+        wave_max(3, mst);
+        float mstD = 0.0f;
         if constexpr (PREP) {
-          fh8 b[2];
-          mkb16(D1v[2 * c], D1v[2 * c + 1], sD1s, b);
-          mma_to(C4{}, b, accD);
+          mstD = state_max<OTM>(D1v);
+          mD1 = fmaxf(mD1, mstD);
+#pragma unroll
+          for (int t = 0; t < OTM; ++t) accD[t] = z4;
         }
-      };
+        const float sD1s = __builtin_ldexpf(1.0f, f16_scale_exp(mstD));
+        auto extra2 = [&](int c) {
+          if constexpr (PREP) {
+            fh8 b[2];
+            mkb16(D1v[2 * c], D1v[2 * c + 1], sD1s, b);
+            mma_to(C4{}, b, accD);
+          }
+        };
 #pragma unroll
-      for (int t = 0; t < OTM; ++t) S[t] = DS1[t];
-      step(C4{}, C2{}, C0{}, jW1t, f16_scale_exp(mst), a.H[1], 0, 1.0f, 0, a.H[1], a.ld[1], OTM, nullptr, false, extra2);
-      const float suD0 = __builtin_amdgcn_ldexpf(1.0f, -(ej[jW1t] + f16_scale_exp(mstD)));
+        for (int t = 0; t < OTM; ++t) S[t] = DS1[t];
+        step(C4{}, C2{}, C0{}, jW1t, f16_scale_exp(mst), a.H[1], 0, 1.0f, 0, a.H[1], a.ld[1], OTM, nullptr, false,
+             extra2);
+        const float suD0 = __builtin_amdgcn_ldexpf(1.0f, -(ej[jW1t] + f16_scale_exp(mstD)));
 #pragma unroll
-      for (int t = 0; t < OTM; ++t) {
-        const f32x4 h = PF[t];
-        H1f[t] = h;
+        for (int t = 0; t < OTM; ++t) {
+          const f32x4 h = PF[t];
+          H1f[t] = h;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) S[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));   // DS_0
-        if constexpr (PREP) {
-          f32x4 e0;
+          for (int i = 0; i < 4; ++i) S[t][i] = acc[t][i] * (su * c_one_minus_sq(h[i]));   // DS_0
+          if constexpr (PREP) {
+            f32x4 e0;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) e0[i] = -2.0f * (accD[t][i] * suD0) * h[i];
-          st4(fa.E0out, a.ld[1], t, e0);
+            for (int i = 0; i < 4; ++i) e0[i] = -2.0f * (accD[t][i] * suD0) * h[i];
+            st4(fa.E0out, a.ld[1], t, e0);
+          }
         }
+      } else {
+#pragma unroll
+        for (int t = 0; t < OTM; ++t) S[t] = DS1[t];
       }
       wave_max(4, state_max<OTM>(S));
       const __amdgpu_buffer_rsrc_t rx = rsrc(a.X, a.ld[0]);
@@ -592,16 +618,16 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], t));
       {
-        // g_W_2 += H_2^T DS_2 (both images written above); g_b_2 from DS_2's f32 tiles
+        // g_W_NH += H_NH^T DS_h (both images written above); g_b_NH from DS_h's f32 tiles
         f32x4 d2[OTM];
-        const __amdgpu_buffer_rsrc_t rd = rsrc(fa.DS, a.ld[3]);
+        const __amdgpu_buffer_rsrc_t rd = rsrc(fa.DS, a.ld[LH]);
 #pragma unroll
-        for (int t = 0; t < OTM; ++t) d2[t] = t < OTA ? ld4(rd, voff(a.ld[3], t)) : z4;
+        for (int t = 0; t < OTM; ++t) d2[t] = t < OTA ? ld4(rd, voff(a.ld[LH], t)) : z4;
         lds_barrier();
-        bias_add(2, COTA{}, d2);
+        bias_add(NH, COTA{}, d2);
         run(dwl, C4{}, COTA{}, 0, eH + eDS);
       }
-      {
+      if constexpr (NH == 2) {
         // g_W_1 += H_1^T DS_1
         lds_barrier();
         const int eg = group_exp(3);
@@ -661,35 +687,40 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
     float mst = state_max<OTM>(RH1);
     wave_max(0, mst);
-    // ---- RH_2 = (1 - H_2^2)(RH_1 W_1 + H_1 V_1 + c_1) ----
+    if constexpr (NH == 2) {
+      // ---- RH_2 = (1 - H_2^2)(RH_1 W_1 + H_1 V_1 + c_1) ----
 #pragma unroll
-    for (int t = 0; t < OTM; ++t) S[t] = RH1[t];
-    step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false, no_extra,
-         FUSED16_REUSE ? H1f : nullptr);
+      for (int t = 0; t < OTM; ++t) S[t] = RH1[t];
+      step(C4{}, C2{}, C2{}, jW1, f16_scale_exp(mst), a.H[1], a.ld[1], sH, eH, a.H[2], a.ld[2], OTM, nullptr, false,
+           no_extra, FUSED16_REUSE ? H1f : nullptr);
 #pragma unroll
-    for (int t = 0; t < OTM; ++t) {
-      const f32x4 cb = bias4(1, t), h = PF[t];
+      for (int t = 0; t < OTM; ++t) {
+        const f32x4 cb = bias4(1, t), h = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) RH2[t][i] = c_one_minus_sq(h[i]) * __builtin_fmaf(acc[t][i], su, cb[i]);
-      H2f[t] = h;
+        for (int i = 0; i < 4; ++i) RH2[t][i] = c_one_minus_sq(h[i]) * __builtin_fmaf(acc[t][i], su, cb[i]);
+        H2f[t] = h;
+      }
+      mst = state_max<OTM>(RH2);
+      wave_max(1, mst);
     }
-    mst = state_max<OTM>(RH2);
-    wave_max(1, mst);
+    // the last hidden layer's R-activations and activations: NH = 2: RH_2, H_2; NH = 1: RH_1, H_1
+    f32x4(&RHt)[OTM] = NH == 2 ? RH2 : RH1;
+    f32x4(&Htf)[OTM] = NH == 2 ? H2f : H1f;
 
-    // ---- R-softmax head; H_2 captured into the act image ----
+    // ---- R-softmax head; H_NH captured into the act image ----
     {
-      const int A = a.w[3];
+      const int A = a.w[LH];
 #pragma unroll
-      for (int t = 0; t < OTM; ++t) S[t] = RH2[t];
-      step(COTA{}, C2{}, C2{}, jW2, f16_scale_exp(mst), a.H[2], a.ld[2], sH, eH, a.P, a.ld[3], 2, sA, false, no_extra,
-           FUSED16_REUSE ? H2f : nullptr);
+      for (int t = 0; t < OTM; ++t) S[t] = RHt[t];
+      step(COTA{}, C2{}, C2{}, NH == 2 ? jW2 : jW1, f16_scale_exp(mst), a.H[NH], a.ld[NH], sH, eH, a.P, a.ld[LH], 2, sA,
+           false, no_extra, FUSED16_REUSE ? Htf : nullptr);
       // R-softmax in f32 on the cancellation-free form of tail.hip / gemm.hip kRHead:
       //   RD_j = (1/N)[Rp_j (B_j - sum p B) + Rp_j A_j^2 + p_j sum_k Rp_k A_k B_k],
       //   Rp = p (Rz - <p, Rz>), A = p / (p + eps), B = eps / (p + eps); the 4 lanes of a state hold 8 actions each
       float zf[8], pf[8], inv[8];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const f32x4 cb = bias4(2, t);
+        const f32x4 cb = bias4(NH, t);
         const f32x4 pv = PF[t];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -732,28 +763,30 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       for (int t = 2; t < OTM; ++t) S[t] = z4;
       mst = state_max<2>(S);
       wave_max(2, mst);
-      // gradient pass: (Hv)_W_2 += H_2^T RD_2  (act captured in the step)
+      // gradient pass: (Hv)_W_NH += H_NH^T RD_h  (act captured in the step)
       lds_barrier();
       const int eg = group_exp(2);
       const float sg = __builtin_ldexpf(1.0f, eg);
 #pragma unroll
       for (int t = 0; t < OTA; ++t) put4(sD, t, S[t], sg);
-      bias_add(2, COTA{}, S);
+      bias_add(NH, COTA{}, S);
       lds_barrier();
       run(dwl, C4{}, COTA{}, 0, eH + eg);
     }
 
-    // ---- R-backward into layer 2's input: RD_1 = (RD_2 W_2^T + D_2 V_2^T)(1 - H_2^2) + E_1 RH_2; D_2 captured ----
-    step(C4{}, C1{}, C1{}, jW2t, f16_scale_exp(mst), a.D[2], a.ld[3], sD2, eD2, a.E[1], a.ld[2], OTM, sD, false, no_extra);
+    // ---- R-backward into the head layer's input: RD_{NH-1} = (RD_h W_NH^T + D_h V_NH^T)(1 - H_NH^2) + E_{NH-1} RH_NH;
+    //      D_h captured ----
+    step(C4{}, C1{}, C1{}, NH == 2 ? jW2t : JW1T, f16_scale_exp(mst), a.D[NH], a.ld[LH], NH == 2 ? sD2 : sD1,
+         NH == 2 ? eD2 : eD1, a.E[NH - 1], a.ld[NH], OTM, sD, false, no_extra);
 #pragma unroll
     for (int t = 0; t < OTM; ++t) {
-      const f32x4 h = H2f[t], e = PF[t];
+      const f32x4 h = Htf[t], e = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH2[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
+      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RHt[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
     }
     mst = state_max<OTM>(S);
-    wave_max(3, mst);
-    {
+    wave_max(NH == 2 ? 3 : 4, mst);
+    if constexpr (NH == 2) {
       // (Hv)_W_2 += RH_2^T D_2 ; H_1 for the next pass is loaded meanwhile
       lds_barrier();
       const int eg = group_exp(1);
@@ -779,18 +812,21 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
       run(dwh, C4{}, C4{}, 0, eH + eg1);
     }
 
-    // ---- R-backward into layer 1's input: RD_0 = (RD_1 W_1^T + D_1 V_1^T)(1 - H_1^2) + E_0 RH_1; D_1 captured ----
-    step(C4{}, C2{}, C2{}, jW1t, f16_scale_exp(mst), a.D[1], a.ld[2], sD1, eD1, a.E[0], a.ld[1], OTM, sD, false, no_extra);
+    if constexpr (NH == 2) {
+      // ---- R-backward into layer 1's input: RD_0 = (RD_1 W_1^T + D_1 V_1^T)(1 - H_1^2) + E_0 RH_1; D_1 captured ----
+      step(C4{}, C2{}, C2{}, jW1t, f16_scale_exp(mst), a.D[1], a.ld[2], sD1, eD1, a.E[0], a.ld[1], OTM, sD, false,
+           no_extra);
 #pragma unroll
-    for (int t = 0; t < OTM; ++t) {
-      const f32x4 h = H1f[t], e = PF[t];
+      for (int t = 0; t < OTM; ++t) {
+        const f32x4 h = H1f[t], e = PF[t];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH1[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
+        for (int i = 0; i < 4; ++i) S[t][i] = __builtin_fmaf(e[i], RH1[t][i], acc[t][i] * (su * c_one_minus_sq(h[i])));
+      }
+      mst = state_max<OTM>(S);
+      wave_max(4, mst);
     }
-    mst = state_max<OTM>(S);
-    wave_max(4, mst);
     {
-      // (Hv)_W_1 += RH_1^T D_1 ; X's first 64 features are loaded meanwhile
+      // (Hv)_W_1 += RH_1^T D_1 (NH = 1: the head layer's, D_1 = D_h) ; X's first 64 features are loaded meanwhile
       lds_barrier();
       const int eg = group_exp(0);
       const float sg = __builtin_ldexpf(1.0f, eg);
@@ -801,7 +837,8 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #pragma unroll
       for (int t = 0; t < OTM; ++t) nxt[t] = ld4(rx, voff(a.ld[0], t));
       lds_barrier();
-      run(dwh, C4{}, C4{}, 0, eg + eD1);
+      if constexpr (NH == 2) run(dwh, C4{}, C4{}, 0, eg + eD1);
+      else run(dwl, C4{}, COTA{}, 0, eg + eD1);
       // (Hv)_W_0 += X^T RD_0 in 64-feature chunks of X
       lds_barrier();
       const int eg0 = group_exp(4);
@@ -871,9 +908,9 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     }
   };
   wout(dw0, 0, TI0, OTM);
-  wout(dwh, 1, OTM, OTM);
-  wout(dwl, 2, OTM, OTA);
-  for (int i = threadIdx.x; i < 3 * 64; i += NT) {
+  if constexpr (NH == 2) wout(dwh, 1, OTM, OTM);
+  wout(dwl, NH, OTM, OTA);
+  for (int i = threadIdx.x; i < (NH + 1) * 64; i += NT) {
     const int m = i >> 6, j = i & 63;
     if (j < a.w[m + 1]) {
       float t = 0.0f;
@@ -899,10 +936,11 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
 #ifndef FWDL16_NW
 #define FWDL16_NW 8   // waves per workgroup (sharing one LDS copy of the weights): C3 0.217 ms at 4, 0.201 at 8
 #endif
-template <int TI0, int OTA, bool PREP>
+template <int TI0, int OTA, bool PREP, int NH>
 __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const FwdLoss16Args a) {
   constexpr int OTM = 4, KX = (TI0 + 1) / 2, NW = FWDL16_NW, NT = 64 * NW;
-  constexpr int NCK = KX + 4;                  // W_0 (KX chunks), W_1 (2), W_2 (2)
+  constexpr int LH = NH + 1;                   // index of the action width in w[] / ld[]
+  constexpr int NCK = KX + 2 * NH;             // W_0 (KX chunks), W_1 (2)[, W_2 (2)]
   constexpr int CHU = 8 * 16 * OTM;            // 16-B units of a full chunk
   __shared__ cu32x4 wl[NCK][CHU];
   __shared__ __attribute__((aligned(16))) float sbias[3][64];
@@ -915,7 +953,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
   }
   for (int i = threadIdx.x; i < 3 * 64; i += NT) {
     const int l = i >> 6, j = i & 63;
-    sbias[l][j] = j < a.w[l + 1] ? a.theta[a.offb[l] + j] : 0.0f;
+    sbias[l][j] = l <= NH && j < a.w[l + 1] ? a.theta[a.offb[l] + j] : 0.0f;
   }
   __syncthreads();
 
@@ -924,11 +962,11 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
   const int eX = __builtin_amdgcn_readfirstlane(amax_exp(a.am_x));
   const int eH = f16_scale_exp(1.0f);
   const int e0 = __builtin_amdgcn_readfirstlane(a.img_e[0]), e1 = __builtin_amdgcn_readfirstlane(a.img_e[1]);
-  const int e2 = __builtin_amdgcn_readfirstlane(a.img_e[2]);
+  const int e2 = NH == 2 ? __builtin_amdgcn_readfirstlane(a.img_e[2]) : 0;
   const float sX = __builtin_ldexpf(1.0f, eX), sH = __builtin_ldexpf(1.0f, eH);
   const float u0 = __builtin_ldexpf(1.0f, -(e0 + eX)), u1 = __builtin_ldexpf(1.0f, -(e1 + eH));
-  const float u2 = __builtin_ldexpf(1.0f, -(e2 + eH));
-  const int A = a.w[3], ld0 = a.ld[0], ldo = a.ld[3];
+  const float u2 = __builtin_ldexpf(1.0f, -((NH == 2 ? e2 : e1) + eH));   // the head layer's
+  const int A = a.w[LH], ld0 = a.ld[0], ldo = a.ld[LH];
   const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 
   // acc[0, OT) += chunk (weights in LDS) x b
@@ -1006,25 +1044,27 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       acc[t] = z4;
     }
     if constexpr (PREP) st_tiles(a.H1, a.ld[1], OTM, H);
+    if constexpr (NH == 2) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        fh8 b[2];
+        mkb16(H[2 * c], H[2 * c + 1], sH, b);
+        mma_chunk(KX + c, C4{}, b, acc);
+      }
+#pragma unroll
+      for (int t = 0; t < OTM; ++t) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[1][16 * t + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u1, bb[i]));
+        acc[t] = z4;
+      }
+      if constexpr (PREP) st_tiles(a.H2, a.ld[2], OTM, H);
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       fh8 b[2];
       mkb16(H[2 * c], H[2 * c + 1], sH, b);
-      mma_chunk(KX + c, C4{}, b, acc);
-    }
-#pragma unroll
-    for (int t = 0; t < OTM; ++t) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[1][16 * t + 4 * g]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) H[t][i] = tanh_fast(__builtin_fmaf(acc[t][i], u1, bb[i]));
-      acc[t] = z4;
-    }
-    if constexpr (PREP) st_tiles(a.H2, a.ld[2], OTM, H);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      fh8 b[2];
-      mkb16(H[2 * c], H[2 * c + 1], sH, b);
-      mma_chunk(KX + 2 + c, COTA{}, b, acc);
+      mma_chunk(KX + 2 * (NH - 1) + c, COTA{}, b, acc);
     }
 
     // ---- softmax and the row terms (rowepi.h kLossHead): lane g holds actions 16t + 4g + i ----
@@ -1042,7 +1082,7 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
       for (int i = 0; i < 4; ++i) {
         const int col = 16 * t + 4 * g + i;
         const bool real = col < A;
-        z[4 * t + i] = real ? __builtin_fmaf(acc[t][i], u2, sbias[2][col]) : -INFINITY;
+        z[4 * t + i] = real ? __builtin_fmaf(acc[t][i], u2, sbias[NH][col]) : -INFINITY;
         oldv[4 * t + i] = a.old[rc * ldo + (real ? col : 0)];
         zm = fmaxf(zm, z[4 * t + i]);
       }
@@ -1124,13 +1164,23 @@ __global__ void __launch_bounds__(64 * FWDL16_NW, 2) fwd_loss16_kernel(const Fwd
 
 int ti0_of(int obs) { return obs <= 16 ? 1 : obs <= 32 ? 2 : obs <= 64 ? 4 : 8; }
 
-template <int TI0, int MODE>
+template <int TI0, int MODE, int NH>
 void launch_ti0(const Fused16Args& a, int grid, hipStream_t s) {
   constexpr int FW = FUSED16_FW, LB = FUSED16_LB;
-  if (a.f.c.w[3] <= 16)
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1, MODE>), dim3(grid), dim3(FW * 64), 0, s, a);
+  if (a.f.c.w[NH + 1] <= 16)
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 1, MODE, NH>), dim3(grid), dim3(FW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2, MODE>), dim3(grid), dim3(FW * 64), 0, s, a);
+    hipLaunchKernelGGL((fvp_fused16_kernel<FW, LB, TI0, 2, MODE, NH>), dim3(grid), dim3(FW * 64), 0, s, a);
+}
+
+template <int MODE, int NH>
+void launch_nh(const Fused16Args& a, int grid, hipStream_t s) {
+  switch (ti0_of(a.f.c.w[0])) {
+    case 1: launch_ti0<1, MODE, NH>(a, grid, s); break;
+    case 2: launch_ti0<2, MODE, NH>(a, grid, s); break;
+    case 4: launch_ti0<4, MODE, NH>(a, grid, s); break;
+    default: launch_ti0<8, MODE, NH>(a, grid, s); break;
+  }
 }
 
 template <int MODE>
@@ -1138,24 +1188,27 @@ void launch_fused16(const Fused16Args& a, int grid, hipStream_t s) {
   constexpr bool PG = MODE >= 1;
   if (grid <= 0) return;
   if (!fused16_eligible(a.f.c.L, a.f.c.w)) throw std::runtime_error("fused16: unsupported shape");
-  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + 14) throw std::runtime_error("fused16: chunk table");
+  const int nh = a.f.c.L - 1;
+  if (a.f.c.nchunks != fused16_obs_chunks(a.f.c.w[0]) + (nh == 2 ? 14 : 6))
+    throw std::runtime_error("fused16: chunk table");
   const int rb = fused16_states_per_group();
   if (a.f.ngroups != (a.f.c.n + rb - 1) / rb) throw std::runtime_error("fused16: group count does not match");
   if (PG && !a.DS) throw std::runtime_error("fused16 policy gradient: no head delta");
-  if (MODE == 2 && (!a.D1out || !a.E1out || !a.E0out)) throw std::runtime_error("fused16 prepare backward: no outputs");
-  switch (ti0_of(a.f.c.w[0])) {
-    case 1: launch_ti0<1, MODE>(a, grid, s); break;
-    case 2: launch_ti0<2, MODE>(a, grid, s); break;
-    case 4: launch_ti0<4, MODE>(a, grid, s); break;
-    default: launch_ti0<8, MODE>(a, grid, s); break;
-  }
+  if (MODE == 2 && (!a.E0out || (nh == 2 && (!a.D1out || !a.E1out))))
+    throw std::runtime_error("fused16 prepare backward: no outputs");
+  if (nh == 2) launch_nh<MODE, 2>(a, grid, s);
+  else launch_nh<MODE, 1>(a, grid, s);
 }
 
 }  // namespace
 
+// one or two tanh hidden layers of width <= 64 (images padded to 64), obs <= 128, <= 32 actions
 bool fused16_eligible(int L, const int* w) {
-  return L == 3 && w[0] >= 1 && w[0] <= 128 && w[1] > 48 && w[1] <= 64 && w[2] > 48 && w[2] <= 64 && w[3] >= 1 &&
-         w[3] <= 32;
+  if (L != 2 && L != 3) return false;
+  if (w[0] < 1 || w[0] > 128 || w[L] < 1 || w[L] > 32) return false;
+  for (int l = 1; l < L; ++l)
+    if (w[l] < 1 || w[l] > 64) return false;
+  return true;
 }
 
 int fused16_obs_chunks(int obs) { return (ti0_of(obs) + 1) / 2; }
@@ -1176,20 +1229,27 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
 void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {
   if (a.n <= 0) return;
   const bool prep = a.H1 != nullptr;
-  if (prep && (!a.H2 || !a.P || !a.D || !a.DS)) throw std::runtime_error("fwd_loss16 prepare: missing output");
-  if (!fused16_eligible(3, a.w)) throw std::runtime_error("fwd_loss16: unsupported shape");
+  const int nh = a.L - 1;
+  if (prep && ((nh == 2 && !a.H2) || !a.P || !a.D || !a.DS)) throw std::runtime_error("fwd_loss16 prepare: missing output");
+  if (!fused16_eligible(a.L, a.w)) throw std::runtime_error("fwd_loss16: unsupported shape");
   const int ti0 = ti0_of(a.w[0]);
-  if (a.nchunks != (ti0 + 1) / 2 + 4) throw std::runtime_error("fwd_loss16: chunk table");
+  if (a.nchunks != (ti0 + 1) / 2 + 2 * nh) throw std::runtime_error("fwd_loss16: chunk table");
   const int64_t waves = (a.n + 15) / 16;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((waves + FWDL16_NW - 1) / FWDL16_NW, (int64_t)num_cus * 2));
-  const bool two = a.w[3] > 16;
-#define FWD_LOSS16(T)                                                                                             \
-  if (prep) {                                                                                                     \
-    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, true>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);     \
-    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, true>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);         \
-  } else {                                                                                                        \
-    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, false>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);    \
-    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, false>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);        \
+  const bool two = a.w[a.L] > 16;
+#define FWD_LOSS16_NH(T, NH)                                                                                       \
+  if (prep) {                                                                                                      \
+    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, true, NH>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);  \
+    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, true, NH>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);      \
+  } else {                                                                                                         \
+    if (two) hipLaunchKernelGGL((fwd_loss16_kernel<T, 2, false, NH>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a); \
+    else hipLaunchKernelGGL((fwd_loss16_kernel<T, 1, false, NH>), dim3(grid), dim3(64 * FWDL16_NW), 0, s, a);     \
+  }
+#define FWD_LOSS16(T)       \
+  if (nh == 2) {            \
+    FWD_LOSS16_NH(T, 2)     \
+  } else {                  \
+    FWD_LOSS16_NH(T, 1)     \
   }
   switch (ti0) {
     case 1: FWD_LOSS16(1) break;
@@ -1198,6 +1258,7 @@ void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {
     default: FWD_LOSS16(8) break;
   }
 #undef FWD_LOSS16
+#undef FWD_LOSS16_NH
 }
 
 void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s) { launch_fused16<0>(a, grid, s); }

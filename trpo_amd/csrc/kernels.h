@@ -43,7 +43,8 @@ struct Options {
                    // fused16: 1 (default) the prepare pass's and the line search's, 2 the line search's only,
                    // 0 neither (per-layer row GEMMs + head_fwd)
   int cg_fuse_reduce;  // engine: single rank with the one-launch FVP: each CG iteration's slab reduction fused with
-                       // its z = Hv + damping p (vec.hip reduce_slab_kernel<true>): 1 (default) on, 0 off
+                       // its z = Hv + damping p (vec.hip reduce_slab_kernel<true>): 1 (default) on, 0 off; the
+                       // p.z partials are grouped differently, so 1 and 0 are not bit-identical to each other
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -393,11 +394,11 @@ bool fused_fvp_eligible(int L, const int* w);
 int fused_fvp_states_per_group(int variant);
 void launch_fvp_fused(const FusedArgs& a, int grid, int variant, hipStream_t s);
 
-// The same one-launch FVP on the f16 split (fused16.hip) for two hidden layers of width 49..64, obs <= 128 and
-// <= 32 actions (C2, C3).  Weight images: the chain's job list (ChainImgJob; kc = fused16_obs_chunks(obs) for
+// The same one-launch FVP on the f16 split (fused16.hip) for one or two hidden layers of width <= 64, obs <= 128
+// and <= 32 actions (C1, C2, C3; hidden dimensions padded to 64 in the images).  Weight images: the chain's job list (ChainImgJob; kc = fused16_obs_chunks(obs) for
 // V_0) as 32-deep chunks of [2 f16 planes (hi, lo)][otp rows][32], each job scaled by a power of two whose
 // exponent launch_fused16_img writes to img_e[job]; jobs in the order V_0 | W_1 V_1 | W_2 V_2 | W_2^T V_2^T |
-// W_1^T V_1^T.  X, D_1 and D_2 are scaled from the engine's running-max slots.
+// W_1^T V_1^T (one hidden layer: V_0 | W_1 V_1 | W_1^T V_1^T; hidden K padded to 2 chunks, hidden O to 64 rows).  X, D_1 and D_2 are scaled from the engine's running-max slots.
 constexpr int kFused16Jobs = 9;
 struct Fused16Args {
   FusedArgs f;                       // f.c.img / f.c.tab / f.c.nchunks: the f16 images and their chunk table
@@ -430,6 +431,7 @@ void launch_prep_pg_fused16(const Fused16Args& a, int grid, hipStream_t s);
 // order here; img_e per job) resident in LDS, one wave per 16 states, no barrier in the loop.
 struct FwdLoss16Args {
   int64_t n;
+  int L = 3;                         // layers (2: one hidden layer, w = [obs, h1, A])
   int w[4], ld[4];                   // widths [obs, h1, h2, A]; row strides
   const float* X;
   const float* theta;                // the trial vector (biases)

@@ -106,7 +106,10 @@ reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* o
         v = (double)pi * (double)zi;
       }
       v = wave_sum_d(v);
-      if (c == 0) partials[blockIdx.x] = v;
+      // the fixed-length partial layout holds kRedBlocks blocks (P <= kRedBlocks x 64, engine.cpp
+      // cg_fused_reduce_ok): a larger grid would write past it, so its extra blocks drop their partial (and the
+      // host refuses such a launch)
+      if (c == 0 && blockIdx.x < kRedBlocks) partials[blockIdx.x] = v;
     }
     if (blockIdx.x == 0)
       for (int i = (int)gridDim.x + threadIdx.x; i < kRedBlocks; i += blockDim.x) partials[i] = 0.0;
