@@ -351,7 +351,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     (4, [64], 2, 1000),                # C1 dims: one hidden layer (the reference policy, trpo_inksci.py:38-40)
     (128, [32], 32, 4099),             # one hidden layer of 32 (padded to 64), two action tiles
     (37, [50, 33], 7, 129),            # hidden widths below 49 (padded images)
-    (16, [17, 48], 17, 1),             # one state, narrow widths
+    (16, [17, 48], 17, 37),            # narrow widths, one partial group
 ])
 def test_fused16_loss_forward_vs_oracle(gpu_available, obs, hidden, A, n):
     """The policy forward in one launch (fused16.hip fwd_loss16, ls_fused = 1) against the float64 oracle and the

@@ -55,6 +55,9 @@
 #ifndef FUSED16_PFEARLY
 #define FUSED16_PFEARLY 1   // 1: a step's epilogue operand is loaded before its register segment, not its memory one
 #endif
+#ifndef FUSED16_DMA
+#define FUSED16_DMA 1   // 1: weight chunks stream by LDS-DMA into a 3-slot ring; 0: through two register sets
+#endif
 
 
 namespace trpo {
@@ -200,11 +203,14 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   constexpr int TWH = (OTM * OTM + FW - 1) / FW;   //                       hidden x hidden
   constexpr int TWL = (OTM * OTA + FW - 1) / FW;   //                       hidden x actions
   constexpr int RING = FUSED16_RING;
-  __shared__ cu32x4 wl[2][CHU];
+  // weight-chunk ring: FUSED16_DMA: three slots, chunk q of a group in slot q % 3 (three distinct objects, so the
+  // compiler's LDS-DMA wait before a slot's first read counts only the DMA into that slot); else two buffers
+  __shared__ cu32x4 wl0[CHU], wl1[CHU], wl2[FUSED16_DMA ? CHU : 1];
   __shared__ __attribute__((aligned(16))) unsigned short simg[2][2 * PL];   // [act | delta] images, hi / lo planes
   __shared__ float sb[FW][3][64];                                          // per-wave bias sums
   __shared__ __attribute__((aligned(16))) float sc[3][64];                // the tangent's biases c_l
   __shared__ float sred[5][FW];                                            // wave maxima: RH1 RH2 RDh RD1 RD0
+  __shared__ int stab[64];   // the chunk table (offset, size), read per chunk from LDS, not by a vector load
 
   const ChainArgs& a = fa.f.c;
   if (a.skip && *a.skip) return;
@@ -215,6 +221,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   unsigned short* const sD = &simg[1][0];
 
   for (int i = threadIdx.x; i < FW * 3 * 64; i += NT) (&sb[0][0][0])[i] = 0.0f;
+  for (int i = threadIdx.x; i < 2 * a.nchunks && i < 64; i += NT) stab[i] = a.tab[i];   // (first read after a barrier)
   for (int i = threadIdx.x; i < 3 * 64; i += NT) {   // (no tangent in the policy gradient)
     const int l = i >> 6, j = i & 63;
     sc[l][j] = !PG && l <= NH && j < a.w[l + 1] ? a.v[a.offb[l] + j] : 0.0f;
@@ -254,9 +261,30 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // image chunk (table index) of the group's chunk q: the FVP streams the whole image, the policy gradient
   // W_2^T (one chunk) and W_1^T (two); with one hidden layer W_1^T (one chunk: K = actions)
   auto chunk_of = [&](int q) { return PG ? (NH == 1 ? KX + 4 : q == 0 ? KX + 8 : KX + 9 + q) : q; };
-  constexpr int WS = FUSED16_WSETS;
+  constexpr int WS = FUSED16_DMA ? 1 : FUSED16_WSETS;
   cu32x4 wr[WS][NLD];
+  // ---- LDS-DMA weight stream (FUSED16_DMA): chunk q of a group is DMA'd into slot q % 3 at chunk q - 2's begin
+  // (after its barrier: every wave is past chunk q - 3, the slot's last reader).  The next group's chunk j (0, 1)
+  // goes to slot j when one of the current group's last two chunks frees it (both do when NCH % 3 == 0: C2, C3),
+  // else at its group's start.  Each wave-instruction moves 1 KB: lanes -> consecutive 16-B units, the image's
+  // own layout. ----
+  auto slot = [&](int k) -> cu32x4* { return k % 3 == 0 ? wl0 : k % 3 == 1 ? wl1 : wl2; };
+  auto dma = [&](int sl, int qq, bool from_lds = true) __attribute__((always_inline)) {
+    const int off = __builtin_amdgcn_readfirstlane(from_lds ? stab[2 * qq] : a.tab[2 * qq]);
+    const int sz = __builtin_amdgcn_readfirstlane(from_lds ? stab[2 * qq + 1] : a.tab[2 * qq + 1]);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int base = wv * 64 + i * NT;   // this wave-instruction's first unit
+      if (CHU % NT != 0 && base >= CHU) break;
+      const int idx = base + (int)(threadIdx.x & 63);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rimg, (__attribute__((address_space(3))) void*)(slot(sl) + base), 16, (idx < sz ? idx : sz - 1) * 16,
+          off * 16, 0, 0);
+    }
+  };
   auto gload = [&](int set, int qq) {
+    if constexpr (FUSED16_DMA) return;
     if constexpr ((FUSED16_ABL & 4) != 0) return;
     if constexpr ((FUSED16_ABL & 16) != 0) {   // no weight loads, but the chunk's LDS stores kept (opaque values)
 #pragma unroll
@@ -276,8 +304,13 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
           cu32x4, __builtin_amdgcn_raw_buffer_load_b128(rimg, (idx < sz ? idx : sz - 1) * 16, off * 16, 0));
     }
   };
+  if constexpr (FUSED16_DMA) {   // (the table's LDS copy is not visible before the first barrier)
+    dma(0, chunk_of(0), false);
+    if constexpr (NCH > 1) dma(1, chunk_of(1), false);
+  } else {
 #pragma unroll
-  for (int k = 0; k < WS; ++k) gload(k, chunk_of(k));
+    for (int k = 0; k < WS; ++k) gload(k, chunk_of(k));
+  }
 
   const int ngroups = fa.f.ngroups;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -291,12 +324,40 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
     const int lrow = wave * 16 + s;
     const int frag = s * 32 + ((g ^ chain_hsw(s)) << 3);
 
-    // ---- weight-chunk stream: chunk q goes to buffer q & 1, one barrier per chunk ----
+    // ---- weight-chunk stream: one barrier per chunk ----
     int q = 0;
     const unsigned short* W = nullptr;   // this lane's A fragment in the current chunk
-    auto chunk_begin = [&]() __attribute__((always_inline)) {
+    if constexpr (FUSED16_DMA) {
+      // the next group's first chunks that the previous group's last chunks could not prefetch
+      if (grp != (int)blockIdx.x) {
+        if constexpr (NCH % 3 == 1) dma(0, chunk_of(0));
+        if constexpr (NCH % 3 == 2) dma(1, chunk_of(1));
+      }
+    }
+    const bool more = grp + (int)gridDim.x < ngroups;   // a next group (uniform)
+    auto chunk_begin_dma = [&]() __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
-      cu32x4* buf = &wl[q & 1][0];
+      cu32x4* buf = slot(q);
+      // this wave's DMA into the slot has landed (the compiler's LDS-DMA wait, placed before this read) ...
+      cu32x4 probe = buf[threadIdx.x];
+      asm volatile("" ::"v"(probe));
+      // ... and every wave's: chunk q visible; every wave is past chunk q - 1 (slot (q + 2) % 3's last reader)
+      lds_barrier();
+      if (q + 2 < NCH) {
+        dma(q + 2, chunk_of(q + 2));
+      } else if ((q + 2) % 3 <= 1 && (q + 2) % 3 < NCH) {   // the next group's chunk (q + 2) % 3, into its slot
+        if (more) dma((q + 2) % 3, chunk_of((q + 2) % 3));
+      }
+      W = reinterpret_cast<const unsigned short*>(buf) + frag;
+      ++q;
+    };
+    auto chunk_begin = [&]() __attribute__((always_inline)) {
+      if constexpr (FUSED16_DMA) {
+        chunk_begin_dma();
+        return;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      cu32x4* buf = slot(q & 1);
 #pragma unroll
       for (int i = 0; i < NLD; ++i) {
         const int idx = threadIdx.x + i * NT;
