@@ -70,6 +70,11 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EPISODE_LEN = 200              # CartPole-v0 cap
 
 CONFIGS = {
+    # BASELINE configs[0] is one CartPole-v0 update on the CPU reference; "c1" is that policy's shape (obs 4, one
+    # 64-wide tanh layer, 2 actions, trpo_inksci.py:38-40) on a device-sized synthetic batch (an A/B line, not the
+    # headline)
+    "c1": dict(n=1_000_000, obs=4, hidden=[64], A=2, cpu_rows=100_000,
+               name="C1 shape: 1M states, obs 4, one 64-wide tanh layer, 2 actions"),
     "c2": dict(n=50_000, obs=11, hidden=[64, 64], A=3, cpu_rows=50_000,
                name="C2: 50k states, obs 11, 64x64 tanh MLP, 3 actions"),
     "c3": dict(n=1_000_000, obs=128, hidden=[64, 64], A=18, cpu_rows=100_000,

@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(FW * 64, LB) fvp_fused16_kernel(const Fused16A
   // own layout. ----
   auto slot = [&](int k) -> cu32x4* { return k % 3 == 0 ? wl0 : k % 3 == 1 ? wl1 : wl2; };
   auto dma = [&](int sl, int qq, bool from_lds = true) __attribute__((always_inline)) {
+    if constexpr ((FUSED16_ABL & 4) != 0) return;   // ablation: no weight-chunk loads
     const int off = __builtin_amdgcn_readfirstlane(from_lds ? stab[2 * qq] : a.tab[2 * qq]);
     const int sz = __builtin_amdgcn_readfirstlane(from_lds ? stab[2 * qq + 1] : a.tab[2 * qq + 1]);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
