@@ -221,8 +221,12 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * is created; "ls_fused" (where the FVP runs on fused16.hip, the policy forward as one launch from f16 weight
  * images, fwd_loss16: 1 = the prepare pass's and the line search's, the default; 2 = the line search's only;
  * 0 = the per-layer forwards); "cg_fuse_reduce" (single rank with the one-launch FVP: each CG iteration's slab
- * reduction fused with its z = Hv + damping p step; 1 = on, the default; 0 = off: the two group the p.z
- * partials differently, so each is deterministic but their CG scalars are not bit-identical to each other).
+ * reduction fused with its z = Hv + damping p step; 1 = on, the default; 2 = on, and the rest of the iteration
+ * (x, r, p, the next FVP's f16 V image) runs in the same launch, in the workgroup that finishes last,
+ * bit-identical to 1 but slower (one CU's serial tail); 0 = off: 0 and 1 group the p.z partials differently, so
+ * each is deterministic but their CG scalars are not bit-identical to each other).
+ * "rfwd01" (the FVP's R-forward through layers 0 and 1 as one launch, rfwd.hip, where two hidden layers of 256
+ * with obs <= 128 run the fused tail: 1 = on, the default; 0 = the plane and row GEMM launches).
  * "ls_fused" = 2 mixes two forwards inside one line search (loss_before from the per-layer forward, the
  * trials' losses from fwd_loss16); it exists for A/B timing and is held to the same parity tests.
  * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed

@@ -290,6 +290,8 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"ls_fused": 0},                                          # the line search's per-layer forward on fused16 shapes
     {"ls_fused": 2},                                          # per-layer prepare forward, one-launch trial forwards
     {"cg_fuse_reduce": 0},                                    # the CG's separate slab reduction on fused16 shapes
+    {"cg_fuse_reduce": 2},                                    # the whole CG iteration after the FVP in one launch
+    {"rfwd01": 0},                                            # R-forward of layers 0 / 1 as two launches (C4 dims)
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -298,7 +300,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
                                            "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
-                                           "splits", "pg_splits", "ls_fused", "cg_fuse_reduce")}
+                                           "splits", "pg_splits", "ls_fused", "cg_fuse_reduce", "rfwd01")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -983,3 +985,123 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
         assert_vec_close(theta, r.theta_new, REL, f"theta hbwd2={mode}")
     assert_vec_close(out[1][0], out[0][0], REL, "dual vs row-GEMM backward g")
     assert_vec_close(out[2][0], out[0][0], REL, "f32 MFMA dual vs row-GEMM backward g")
+
+
+@pytest.mark.parametrize("obs,hidden,A,n", [
+    (11, [64, 64], 3, 50_000),         # C2: the CG step builds the next FVP's V images
+    (128, [64, 64], 18, 20_000),       # C3 dims: P = 13,586, 213 reduction blocks
+    (4, [64], 2, 1000),                # C1 dims: one hidden layer
+    (37, [50, 33], 7, 129),            # padded widths, one FVP workgroup
+])
+def test_cg_step_one_launch_bitwise(gpu_available, obs, hidden, A, n):
+    """cg_fuse_reduce = 2 (the iteration's x / r / p updates and the next V image in the slab reduction's launch,
+    run by the workgroup that arrives last) is bit-identical to cg_fuse_reduce = 1 (the default, three more launches): the CG
+    solution at residual_tol 0 and with an early exit (utils.py:199-200), and whole updates, eager and replayed
+    from the captured graph."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(obs, hidden, A)
+    dd = O.synthetic_batch(spec, n, seed=31)
+    b = np.random.RandomState(32).standard_normal(spec.n_params).astype(np.float32)
+    dflt = get_option("cg_fuse_reduce")
+    runs = {}
+    try:
+        for mode in (1, 2):
+            set_option("cg_fuse_reduce", mode)
+            e = Engine(obs, hidden, A, max_rows=n)
+            e.set_flat(dd["theta"])
+            e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            x0, it0 = e.cg(b, cg_iters=10, residual_tol=0.0)
+            out = {"x0": x0, "it0": it0}
+            bb = float(np.dot(b.astype(np.float64), b))
+            for f in (0.5, 1e-2, 1e-4):   # early exits after the p update (utils.py:199-200)
+                out[f"x{f}"], out[f"it{f}"] = e.cg(b, cg_iters=10, residual_tol=bb * f)
+            for u in range(3):   # eager, capture, replay
+                e.set_flat(dd["theta"])
+                st = e.update(UpdateParams(residual_tol=1e-3 if u == 2 else 0.0))
+                out[f"theta{u}"] = e.get_flat()
+                out[f"stepdir{u}"] = e.get_vector(3)
+                out[f"iters{u}"] = st["cg_iters"]
+            runs[mode] = out
+            e.close()
+    finally:
+        set_option("cg_fuse_reduce", dflt)
+    for k, v in runs[1].items():
+        if isinstance(v, np.ndarray):
+            assert np.array_equal(v, runs[2][k]), (k, float(np.abs(v - runs[2][k]).max()))
+        else:
+            assert v == runs[2][k], (k, v, runs[2][k])
+    ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], b.astype(np.float64), spec)
+    assert np.all(np.isfinite(ref)) and runs[2]["it0"] == 10
+    assert min(runs[2][f"it{f}"] for f in (0.5, 1e-2, 1e-4)) < 10   # an early exit was exercised
+
+
+def _block_slices(spec):
+    """(W_l, b_l) flat slices in the reference's order [W1, b1, W2, b2, ...] (trpo_inksci.py:49)."""
+    w = [spec.obs_dim] + list(spec.hidden) + [spec.n_actions]
+    out, o = [], 0
+    for l in range(len(w) - 1):
+        out.append((slice(o, o + w[l] * w[l + 1]), slice(o + w[l] * w[l + 1], o + w[l] * w[l + 1] + w[l + 1])))
+        o += w[l] * w[l + 1] + w[l + 1]
+    return out
+
+
+@pytest.mark.parametrize("n,case", [
+    (1, "plain"), (129, "plain"), (1000, "plain"), (40_000, "plain"),   # one state, partial tiles, many tiles
+    (3001, "v0_big"), (3001, "v0_small"),        # RH1 W1 dominant / H1 V1 dominant in the shared exponent
+    (3001, "tanh_sat"),                           # saturated first layer: 1 - H1^2 near 0
+    (3001, "mixed"),       # a few states per 32 with RH1 2^15 larger than their neighbours' (W_0's last rows zero,
+                           # those states' X large there only: X W_0 exact, H1 unsaturated)
+    (3001, "illcond"),     # whole X rows 2^12 larger: X W_0 ill-conditioned for any float32 evaluation
+])
+def test_rfwd01_vs_two_launches_and_oracle(gpu_available, n, case):
+    """The one-launch R-forward of layers 0 / 1 (rfwd.hip) at C4 widths: Hv against the float64 oracle and against
+    the two-launch path (rfwd01 = 0) at 1e-5, in the regimes its per-tile product exponent has to cover."""
+    from trpo_amd import Engine
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(128, [256, 256], 18)
+    dd = O.synthetic_batch(spec, n, seed=41)
+    th = dd["theta"].astype(np.float32).copy()
+    X = dd["X"].astype(np.float32).copy()
+    v = np.random.RandomState(42).standard_normal(spec.n_params).astype(np.float32)
+    (w0, b0), (w1, b1), _ = _block_slices(spec)
+    if case == "v0_big":
+        v[w0] *= 100.0
+        v[b0] *= 100.0
+    elif case == "v0_small":
+        v[w0] *= 1e-3
+        v[b0] *= 1e-3
+    elif case == "tanh_sat":
+        th[w0] *= 20.0
+    elif case == "mixed":
+        th64 = th.astype(np.float64)
+        W0 = th64[w0].reshape(spec.obs_dim, spec.hidden[0])
+        W0[-3:, :] = 0.0
+        th[w0] = W0.reshape(-1).astype(np.float32)
+        rs = np.random.RandomState(43)
+        for i in range(5, n, 29):
+            X[i, -3:] = (2.0 ** 15 * rs.standard_normal(3)).astype(np.float32)
+    elif case == "illcond":
+        X[::97] *= 4096.0
+    # (Hv does not read pi_old or the actions: KL_ff compares p with itself at the same theta, trpo_inksci.py:56-58)
+    dflt = get_option("rfwd01")
+    hv = {}
+    try:
+        for mode in (1, 0):
+            set_option("rfwd01", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(th)
+            e.set_batch(X, dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
+            hv[mode] = e.fvp(v, 0.0)
+            e.close()
+    finally:
+        set_option("rfwd01", dflt)
+    ref = O.fvp_undamped(th.astype(np.float64), X.astype(np.float64), v.astype(np.float64), spec)
+    # 1e-5 wherever float32 arithmetic can meet it: max(1e-5, 4 x the float32 graph's own error) per block
+    # (test_gpu_fused16_hard.py); only "illcond" needs the 4x
+    ref32 = O.fvp_undamped(th, X, v, spec, dtype=np.float32)
+    for sl in [s_ for blk in _block_slices(spec) for s_ in blk]:
+        bar = max(REL, 4.0 * rel_l2(ref32[sl], ref[sl]))
+        assert rel_l2(hv[1][sl], ref[sl]) <= bar, (case, rel_l2(hv[1][sl], ref[sl]), rel_l2(hv[0][sl], ref[sl]), bar)
+    if case != "illcond":
+        assert_vec_close(hv[1], hv[0], REL, f"rfwd01 {case} vs two launches")

@@ -24,6 +24,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// wave_sum_d's butterfly (partners l ^ 32, 16, 8, 4, 2, 1 in that order) on lane-crossing moves instead of
+// ds_bpermute pairs: bit-identical on every lane.  Before the ^8 step every value depends on l mod 16 only, so a
+// rotate by 8 inside the 16-lane row reaches an equal partner; likewise l mod 8 for ^4 (rotate by 4).
+__device__ __forceinline__ double wave_sum_d_fast(double v);
+
 // Block-wide sum in a fixed order (wave shuffles, then waves in index order).
 // Every thread returns the total.  `scratch` must hold blockDim.x/64 doubles.
 __device__ __forceinline__ double block_sum_d(double v, double* scratch) {
@@ -121,6 +126,15 @@ __device__ __forceinline__ float max32_dpp(float v) {
   v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
   v = fmaxf(v, dpp_f<kDppMirror>(v));
   return xmax_f<false>(v);
+}
+
+__device__ __forceinline__ double wave_sum_d_fast(double v) {
+  v = xadd_d<true>(v);
+  v = xadd_d<false>(v);
+  v += dpp_d<0x128>(v);   // row_ror:8
+  v += dpp_d<0x124>(v);   // row_ror:4
+  v += dpp_d<0x4E>(v);    // quad xor 2
+  return v + dpp_d<0xB1>(v);   // quad xor 1
 }
 
 // Workgroup barrier for an LDS hand-off only: waits for this wave's LDS operations,

@@ -186,6 +186,8 @@ struct trpo_engine {
   uint16_t* f16_img = nullptr;
   int* f16_tab = nullptr;
   int* f16_e = nullptr;
+  bool f16_v_img_ready = false;   // cg(): the V images of the next fvp_fused16 were built by the CG step launch
+  unsigned* cg_ticket = nullptr;  // cg_step_slabs_kernel's arrival ticket (zero between launches)
   int f16_nchunks = 0;
   bool f16_w_valid = false;     // theta parts of the f16 images match theta
   ChainImgArgs f16_jobs{};
@@ -198,6 +200,12 @@ struct trpo_engine {
   bool use_fused16() const { return g_options.fused == 3 && f16 && f16_img && fused16_eligible(L, w.data()); }
   // layer 1's R-backward (and the policy gradient's backward into layer 0) fused with layer 0's weight
   // gradient (rbwd0.hip): f16 split with X's planes, obs <= 128, first hidden width <= 256
+  uint16_t* rf_img = nullptr;   // rfwd.hip's chunk image (V0^T, W1, V1 in the kernel's LDS order), per FVP
+  // the R-forward through layers 0 and 1 in one launch: X's planes, the fused tail (RZ2 is its pre-activation)
+  bool use_rfwd01() const {
+    return g_options.rfwd01 != 0 && rf_img && f16 && split_on() && use_tail() && planes_l0() &&
+           rfwd01_eligible(L, w.data(), wp.data()) && (int64_t)x_mpad <= ((int64_t)1 << 23);
+  }
   bool use_rbwd0() const {
     return g_options.rbwd0 != 0 && f16 && x_planes && rbwd0_geom() && g_options.planes != 0 && split_on() &&
            rowgemm_uses_split(wp[1], RowEpi::kRBwd);
@@ -426,10 +434,12 @@ struct trpo_engine {
     scan_ws = dalloc<uint8_t>(discount_workspace_bytes(cap));
     sc = dalloc<UpdScalars>(1);
     fl = dalloc<CGFlags>(1);
+    cg_ticket = dalloc<unsigned>(1);
     dbad = dalloc<int>(1);
     f16 = g_options.split_f16 != 0;
     amax = dalloc<unsigned>((size_t)(1 + 8 * kMaxLayers) * kAmaxSlot);
     if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
+    if (rfwd01_eligible(L, w.data(), wp.data())) rf_img = dalloc<uint16_t>(rfwd01_img_bytes() / 2);
     // allocated last: the big activation buffers keep the placement the kernels were tuned on
     stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     if (f16 && (planes_geom_l0() || rbwd0_geom())) {
@@ -1252,7 +1262,40 @@ struct trpo_engine {
     // R-forward (the fused tail takes the last layer's)
     const bool tail = use_tail();
     const int Lf = tail ? L - 1 : L;
-    for (int l = 0; l < Lf; ++l) {
+    int l_first = 0;
+    if (use_rfwd01()) {   // layers 0 and 1 in one launch (rfwd.hip): RH1 and the tail's RZ2
+      {
+        Scope sp(this, "fvp_rfwd_img");
+        launch_rfwd01_img(theta, v, offW[0], offW[1], w[0], am_v(0), am_w(1), am_v(1), rf_img, skip, stream);
+        check_launch();
+      }
+      Rfwd01Args ra{};
+      ra.n = n;
+      ra.obs = w[0];
+      ra.ldh = wp[1];
+      ra.ldz = wp[2];
+      ra.Xh = Xh;
+      ra.Xl = Xl;
+      ra.x_mpad = x_mpad;
+      ra.eX = pl_e;
+      ra.H1 = H[1];
+      ra.c0 = v + offb[0];
+      ra.c1 = v + offb[1];
+      ra.RH1 = RH[1];
+      ra.RZ2 = RH[2];
+      ra.img = rf_img;
+      ra.am_v0 = am_v(0);
+      ra.am_w1 = am_w(1);
+      ra.am_v1 = am_v(1);
+      ra.am_rh1 = am_rh(1);
+      ra.am_rz2 = am_rh(2);
+      ra.skip = skip;
+      Scope sp(this, "fvp_rfwd01");
+      launch_rfwd01(ra, num_cus, stream);
+      check_launch();
+      l_first = 2;
+    }
+    for (int l = l_first; l < Lf; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       float* Vpart = WF[l] + (size_t)wp[l] * wp[l + 1];
       if (l == 0) {
@@ -1514,11 +1557,12 @@ struct trpo_engine {
   // the whole Hv in one launch on the f16 split (fused16.hip) + the slab reduction
   void fvp_fused16(const float* v, float* out, const int* skip, int* defer = nullptr) {
     fused16_w_images();
-    {
+    if (!f16_v_img_ready) {   // else the previous CG step's launch built v's images (cg())
       Scope sp(this, "fvp_img_v");
       launch_fused16_img(f16_jobs, theta, v, 1, skip, f16_e, stream);
       check_launch();
     }
+    f16_v_img_ready = false;
     int grid = 1;
     const Fused16Args fa = fused16_args(v, skip, grid);
     {
@@ -1601,14 +1645,26 @@ struct trpo_engine {
     prepare();
     launch_cg_init(b, xo, r, p, P, partA, sc, fl, tol, damping, stream);
     check_launch();
+    f16_v_img_ready = false;
     for (int it = 0; it < iters; ++it) {
       int slabs = 0;
       fvp(p, hv, &fl->done[it], g_options.cg_fuse_reduce ? &slabs : nullptr);
       Scope sp(this, "cg_vec");
-      if (slabs > 0) launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
-      else launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      if (slabs > 0 && g_options.cg_fuse_reduce == 2) {
+        // the rest of the iteration in the slab reduction's launch; on the fused16 path it also builds the next
+        // iteration's V image, which that FVP then does not launch (fvp_fused16)
+        const CgStepArgs ca{slab, slabs, it, slab_stride, P, hv, xo, r, p, z, sc, partA, fl, cg_ticket};
+        const bool img = use_fused16() && it + 1 < iters;
+        launch_cg_step_slabs(ca, img ? &f16_jobs : nullptr, f16_e, stream);
+        f16_v_img_ready = img;
+      } else if (slabs > 0) {
+        launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      } else {
+        launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+      }
       check_launch();
     }
+    f16_v_img_ready = false;
   }
 
   void fetch_scalars() {
@@ -2712,6 +2768,7 @@ static int* option_slot(const std::string& k) {
   if (k == "pg_splits") return &g_options.pg_splits;
   if (k == "ls_fused") return &g_options.ls_fused;
   if (k == "cg_fuse_reduce") return &g_options.cg_fuse_reduce;
+  if (k == "rfwd01") return &g_options.rfwd01;
   throw ArgError("unknown option " + k);
 }
 

@@ -43,8 +43,12 @@ struct Options {
                    // fused16: 1 (default) the prepare pass's and the line search's, 2 the line search's only,
                    // 0 neither (per-layer row GEMMs + head_fwd)
   int cg_fuse_reduce;  // engine: single rank with the one-launch FVP: each CG iteration's slab reduction fused with
-                       // its z = Hv + damping p (vec.hip reduce_slab_kernel<true>): 1 (default) on, 0 off; the
-                       // p.z partials are grouped differently, so 1 and 0 are not bit-identical to each other
+                       // its z = Hv + damping p (vec.hip reduce_slab_kernel<true>): 1 (default) on, 0 off; the p.z
+                       // partials are grouped differently, so 1 and 0 are not bit-identical to each other; 2 the
+                       // rest of the iteration and the next V image in the same launch, run by the workgroup that
+                       // finishes last (cg_step_slabs_kernel, bit-identical to 1; measured slower: DESIGN.md §6)
+  int rfwd01;          // engine: the FVP's R-forward through layers 0 and 1 in one launch (rfwd.hip) where eligible
+                       // (two hidden layers of 256, obs <= 128, the fused tail, X planes): 1 (default) on, 0 off
 };
 
 // A running-max slot is kAmaxSub counters, each on its own 128-B line: producers reduce within the
@@ -264,6 +268,22 @@ bool cg_fused_reduce_ok(int64_t P);
 void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, float* x, float* r, float* p, float* z,
                           int64_t n, UpdScalars* sc, double* partials, double* partials2, CGFlags* fl, int it,
                           hipStream_t s);
+// cg_fuse_reduce = 2: the whole iteration in one launch (vec.hip cg_step_slabs_kernel): the slab reduction and
+// z / p.z as above, then, in the workgroup that finishes last (an agent-scope ticket that it resets), the x / r and
+// p updates of launch_cg_iter_slabs with bit-identical results, and, when `img` has jobs (the fused16 path), the next
+// FVP's V images and exponents (launch_fused16_img(..., which = 1) of the new p)
+struct CgStepArgs {
+  const float* slab;
+  int S, it;
+  int64_t stride, P;
+  float *hv, *x, *r, *p, *z;
+  UpdScalars* sc;
+  double* partials;
+  CGFlags* fl;
+  unsigned* ticket;   // zero between launches
+};
+struct ChainImgArgs;
+void launch_cg_step_slabs(const CgStepArgs& a, const ChainImgArgs* img, int* img_e, hipStream_t s);
 struct CGScalarsD {
   double rdotr[2];
   double alpha, mu;
@@ -591,6 +611,28 @@ struct HeadFwdArgs {
 bool head_fwd_eligible(int A, int K);
 void launch_head_fwd(const HeadFwdArgs& a, int num_cus, hipStream_t s);
 void launch_head_bwd2(const HeadBwd2Args& a, int num_cus, hipStream_t s);
+// The R-forward through layers 0 and 1 in one launch (rfwd.hip, option rfwd01): RH1 = (1 - H1^2)(X V0 + c0)
+// (stored) and RZ2 = RH1 W1 + H1 V1 + c1 (stored, the fused tail's pre-activation) for two hidden layers of 256
+// and obs <= 128, X from its pre-split planes, V0 / W1 / V1 from a per-FVP chunk image (launch_rfwd01_img).
+struct Rfwd01Args {
+  int64_t n;
+  int obs, ldh, ldz;                 // obs; row strides of H1 / RH1 and of RZ2 (floats)
+  const uint16_t *Xh, *Xl;           // X's k-blocked f16 planes (GemmSeg::Ah), x_mpad rows per 32-k block
+  int x_mpad;
+  const int* eX;                     // their scale exponent
+  const float *H1, *c0, *c1;         // H1; the tangent biases of layers 0 and 1 (v + offb[l])
+  float *RH1, *RZ2;
+  const uint16_t* img;               // rfwd01_img_bytes()
+  const unsigned *am_v0, *am_w1, *am_v1;   // the images' running-max slots
+  unsigned *am_rh1, *am_rz2;         // running max |RH1|, |RZ2| (atomicMax'd)
+  const int* skip;
+};
+bool rfwd01_eligible(int L, const int* w, const int* wp);
+size_t rfwd01_img_bytes();
+void launch_rfwd01_img(const float* theta, const float* v, int64_t offV0, int64_t offW1, int obs,
+                       const unsigned* am_v0, const unsigned* am_w1, const unsigned* am_v1, uint16_t* img,
+                       const int* skip, hipStream_t s);
+void launch_rfwd01(const Rfwd01Args& a, int num_cus, hipStream_t s);
 bool rbwd0_eligible(int obs_pad, int x_ldp, int hid_pad, int K);
 void launch_rbwd0(const RBwd0Args& a, hipStream_t s);
 void launch_tail_pack(const TailPackArgs& p, hipStream_t s);

@@ -1,0 +1,381 @@
+// The FVP's R-forward through the first two layers in one launch (gfx950 / CDNA4): trpo_inksci.py:56-70 (the
+// R-operator of the policy forward, trpo_inksci.py:38-40; SURVEY.md Appendix A "R-forward"), at the C4 shape
+// (two hidden layers of 256, obs <= 128, the fused tail on the head layer):
+//
+//   RZ1 = X V0 + c0 ;  RH1 = (1 - H1^2) RZ1 ;  RZ2 = RH1 W1 + H1 V1 + c1
+//
+// It replaces fvp_rfwd_l0 (plane.hip, writes RH1) + fvp_rfwd_l1 (gemm.hip rowgemm3, reads RH1 and H1 back):
+// RH1 is still written (the layer-1 R-backward's E_0 RH1 term and the layer-1 weight gradient read it), but it
+// is not read back, and H1 is read once.  Bytes per state: X's f16 planes 512 + H1 1024 + RH1 1024 + RZ2 1024 =
+// 3584 (the two launches: 5632).
+//
+// Layout: one workgroup of 8 waves per CU (persistent over 256-state tiles); wave w owns 32 states of the tile
+// and all 256 output columns (128 accumulator registers).  For each 32-feature slice t of layer 1:
+//  * phase A: RZ1^T[32 features x 32 states] = V0^T X^T on v_mfma_f32_32x32x16_f16 (V0^T from LDS as the A
+//    operand, X's pre-split f16 planes from HBM / L2 as the B operand), 3 products;
+//  * epilogue: the accumulator lane holds one state and features 8j + 4h + i (j, i = 0..3, h = lane / 32): RH1
+//    and H1 in that layout are exactly the A operand of the next product with its k order permuted (k-step u
+//    takes registers 8u..8u+7), so RH1 never leaves registers on its way to the second GEMM;
+//  * phase B: RZ2[32 states x 256] += RH1_t W1_t + H1_t V1_t (W1 / V1 rows of slice t, k-permuted the same way,
+//    from LDS as B operands), 3 products per segment.
+// Weights stream through a 4-slot LDS ring by LDS-DMA (24 chunks per tile: V0^T slice t 16 KB, then W1 / V1
+// rows of slice t for output columns 0-127 and 128-255, 32 KB each), built once per FVP in that order by
+// rfwd01_img_kernel (pre-swizzled: the DMA is a straight copy).  Each chunk is DMA'd three chunks ahead.
+//
+// Scales (f16 hi + lo split, kernels.h f16_scale_exp): X from its plane exponent, V0 / W1 / V1 from their
+// running-max slots; RH1 (made in the launch) per state and slice from the state's max |RH1_t| (an A-operand row
+// is one state, so each state has its own exponent), H1 fixed (|h| <= 1).  Both phase-B segments share a state's
+// product exponent, the smaller of the two segments' (and of every earlier slice's); a state's accumulator row
+// steps down by an exact power of two in the rare case a later slice needs it, and is unscaled at the end.
+#include "chain_common.h"
+#include "rowepi.h"
+
+#include <stdexcept>
+
+namespace trpo {
+namespace {
+
+typedef __fp16 rf_h2 __attribute__((ext_vector_type(2)));
+
+constexpr int kRfUnits = 2048;                 // 16-B units of a ring slot / image chunk (32 KB)
+constexpr int kRfChunks = 24;                  // chunks per tile
+constexpr int kRfLd = 256;                     // row stride of H1 / RH1 / RZ2 (floats; launch_rfwd01 checks)
+constexpr int kRfTile = 128, kRfWaves = 4;   // 4 waves of 32 states: 512 registers per wave
+
+// 8 values times s -> f16 hi and lo (round toward zero; x - hi is exact): fused16.hip split2 per pair
+__device__ __forceinline__ void rf_split8(const float* x, float s, f16x8& hi, f16x8& lo) {
+  cu32x4 H, L;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = x[2 * q] * s, b = x[2 * q + 1] * s;
+    const rf_h2 hp = __builtin_amdgcn_cvt_pkrtz(a, b);
+    const rf_h2 lp = __builtin_amdgcn_cvt_pkrtz(a - (float)hp[0], b - (float)hp[1]);
+    H[q] = __builtin_bit_cast(unsigned, hp);
+    L[q] = __builtin_bit_cast(unsigned, lp);
+  }
+  hi = __builtin_bit_cast(f16x8, H);
+  lo = __builtin_bit_cast(f16x8, L);
+}
+
+// c += a b on the split, smallest terms first
+__device__ __forceinline__ f32x16 rf_mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl,
+                                           f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  return c;
+}
+
+// ---- the chunk image (one per FVP: V0 and V1 change, W1 does not within an update) --------------------------
+// chunk 3t (A_t, 16 KB): [plane][feature f 0..31][unit u ^ (f & 15)] with unit u = 2 ks + h holding V0[obs 16 ks
+//   + 8 h + q][32 t + f], q = 0..7 (obs >= the real obs: 0);
+// chunk 3t + 1 + nh (B_t,nh, 32 KB): [matrix W1, V1][plane][column r 0..127][unit u ^ ((r >> 2) & 3)] with unit
+//   u = 2 uu + h holding M[32 t + 16 uu + 4 h + 8 (q >> 2) + (q & 3)][128 nh + r], q = 0..7 (the phase-B k order).
+__global__ void __launch_bounds__(256) rfwd01_img_kernel(const float* __restrict__ theta, const float* __restrict__ v,
+                                                         int64_t offV0, int64_t offW1, int obs,
+                                                         const unsigned* am_v0, const unsigned* am_w1,
+                                                         const unsigned* am_v1, uint16_t* __restrict__ img,
+                                                         const int* skip) {
+  if (skip && *skip) return;
+  const int eV0 = amax_exp(am_v0), eW = amax_exp(am_w1), eV = amax_exp(am_v1);
+  const int gid = blockIdx.x * 256 + threadIdx.x;   // 8 slices x (512 A units + 2 x 1024 B units)
+  const int t = gid / 2560, rem = gid % 2560;
+  if (t >= 8) return;
+  float x[8];
+  cu32x4* dst;
+  int plane_units;
+  float sc;
+  if (rem < 512) {   // A_t: feature f, unit u
+    const int f = rem >> 4, u = rem & 15, ks = u >> 1, h = u & 1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 16 * ks + 8 * h + q;
+      x[q] = k < obs ? v[offV0 + (int64_t)k * 256 + 32 * t + f] : 0.0f;
+    }
+    sc = __builtin_ldexpf(1.0f, eV0);
+    dst = reinterpret_cast<cu32x4*>(img) + (size_t)(3 * t) * kRfUnits + f * 16 + (u ^ (f & 15));
+    plane_units = 512;
+  } else {   // B_t,nh: matrix m, column r, unit u
+    const int b = rem - 512, nh = b >> 10, m = (b >> 9) & 1, r = (b >> 2) & 127, u = b & 3, uu = u >> 1, h = u & 1;
+    const float* src = m ? v : theta;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 32 * t + 16 * uu + 4 * h + 8 * (q >> 2) + (q & 3);
+      x[q] = src[offW1 + (int64_t)k * 256 + 128 * nh + r];
+    }
+    sc = __builtin_ldexpf(1.0f, m ? eV : eW);
+    dst = reinterpret_cast<cu32x4*>(img) + (size_t)(3 * t + 1 + nh) * kRfUnits + m * 1024 + r * 4 +
+          (u ^ ((r >> 2) & 3));
+    plane_units = 512;
+  }
+  f16x8 hi, lo;
+  rf_split8(x, sc, hi, lo);
+  dst[0] = __builtin_bit_cast(cu32x4, hi);
+  dst[plane_units] = __builtin_bit_cast(cu32x4, lo);
+}
+
+template <int KS0>   // 16-deep k-steps over obs (obs <= 16 KS0)
+__global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Args a) {
+  __shared__ cu32x4 q0[kRfUnits], q1[kRfUnits], q2[kRfUnits], q3[kRfUnits];   // the ring: chunk c in slot c % 4
+  __shared__ float red[3][16];
+  __shared__ int pex[kRfWaves][32];   // per-state exponents, from the A-operand lanes to the accumulator lanes
+  if (a.skip && *a.skip) return;
+  const int tid = threadIdx.x, lane = tid & 63, s = lane & 31, h = lane >> 5;
+  const int eX = __builtin_amdgcn_readfirstlane(*a.eX);
+  const int eV0 = __builtin_amdgcn_readfirstlane(amax_exp(a.am_v0));
+  const int eW = __builtin_amdgcn_readfirstlane(amax_exp(a.am_w1));
+  const int eV = __builtin_amdgcn_readfirstlane(amax_exp(a.am_v1));
+  const float uA = __builtin_ldexpf(1.0f, -(eX + eV0));
+  const int64_t ntiles = (a.n + kRfTile - 1) / kRfTile;
+  const __amdgpu_buffer_rsrc_t rimg =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, kRfChunks * kRfUnits * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxh = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xh, 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxl = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xl, 0, 0x7ffffff0, 0x00020000);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Ordering rule: vector-memory returns retire in issue order, so a wait for an ordinary load also waits for every
+  // DMA issued before it.  Each chunk therefore issues its ordinary loads (the next X / H1, c0) BEFORE its DMA, and
+  // the DMA three chunks ahead never stands in front of a load the current chunk consumes.
+  auto slot = [&](int k) -> cu32x4* { return k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3; };
+  // chunk c (0..23) of the image into slot sl (= c % 4): 1 KB per wave-instruction, lane-linear
+  auto dma = [&](int c, int sl) __attribute__((always_inline)) {
+    const int units = c % 3 == 0 ? 1024 : 2048;
+#pragma unroll
+    for (int i = 0; i < 2048 / (kRfWaves * 64); ++i) {
+      const int base = wv * 64 + i * kRfWaves * 64;
+      if (base < units)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rimg, (__attribute__((address_space(3))) void*)(slot(sl) + base),
+                                                 16, (base + lane) * 16, c * kRfUnits * 16, 0, 0);
+    }
+  };
+  // this wave's DMA into slot sl has landed (the compiler's wait before the probe read), then every wave's
+  // (barrier: the chunk is visible, and every wave is past the previous chunk, whose slot is the next DMA's)
+  auto arrive = [&](int sl) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    const cu32x4 probe = slot(sl)[tid];
+    asm volatile("" ::"v"(probe));
+    lds_barrier();
+  };
+  // the DMA three chunks after chunk c (c + 3 < 24: this tile's; else the next tile's, if this workgroup has one)
+  auto ahead = [&](int c, int sl, bool more) __attribute__((always_inline)) {
+    if (c + 3 < kRfChunks) dma(c + 3, (sl + 3) % 4);
+    else if (more) dma(c + 3 - kRfChunks, (sl + 3) % 4);
+  };
+  // X's f16 planes, all k-steps, of one state (B operand: lane (state s, half h) holds obs 16 ks + 8 h .. + 7)
+  // (row0 = the wave's first state: uniform, so every load is one lane offset + one scalar offset)
+  const unsigned xlane = (unsigned)(s * 32 + 8 * h) * 2u;
+  auto xload = [&](int64_t row0, f16x8 (&x)[KS0][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < KS0; ++ks) {
+      const int so = (int)((((unsigned)(ks >> 1) * (unsigned)a.x_mpad + (unsigned)row0) * 32u + 16u * (ks & 1)) * 2u);
+      x[ks][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rxh, xlane, so, 0));
+      x[ks][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rxl, xlane, so, 0));
+    }
+  };
+  const unsigned hlane = (unsigned)(s * kRfLd + 4 * h) * 4u;   // H1 / RH1 rows: lane part of the offset
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)a.c0, 0, 256 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.c1, 0, 256 * 4, 0x00020000);
+  // H1's slice t of one wave's 32 states (rows past n read 0)
+  auto hload = [&](int64_t r0w, int t, float (&hv)[16]) __attribute__((always_inline)) {
+    const int rows = (int)(a.n - r0w < 32 ? (a.n - r0w > 0 ? a.n - r0w : 0) : 32);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.H1 + r0w * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v4 =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, hlane, (32 * t + 8 * j) * 4, 0));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hv[4 * j + i] = v4[i];
+    }
+  };
+
+  f16x8 xt[KS0][2];   // X of this wave's 32 states, the whole tile
+  float hn[16];       // H1 of the next slice, loaded one slice ahead
+  if ((int64_t)blockIdx.x < ntiles) {
+    xload((int64_t)blockIdx.x * kRfTile + wv * 32, xt);
+    hload((int64_t)blockIdx.x * kRfTile + wv * 32, 0, hn);
+  }
+  dma(0, 0);
+  dma(1, 1);
+  dma(2, 2);
+
+  float mR = 0.0f, mZ = 0.0f;   // running max |RH1|, |RZ2| of this lane
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool more = tile + gridDim.x < ntiles;
+    const int64_t r0 = tile * kRfTile + wv * 32;   // this wave's first state (wave-uniform: the buffer bases)
+    const int64_t r0n = r0 + (int64_t)gridDim.x * kRfTile;     // ... in the next tile
+    const int rows = (int)(a.n - r0 < 32 ? (a.n - r0 > 0 ? a.n - r0 : 0) : 32);
+    const __amdgpu_buffer_rsrc_t rrh =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.RH1 + r0 * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
+    f32x16 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = f32x16{};
+    int Ps = 0;   // this lane's state's product exponent (set by slice 0, lowered when a later slice needs it)
+    // accumulator register r of this lane holds state 8 (r >> 2) + 4 h + (r & 3): its exponent comes through LDS
+    int* px = pex[__builtin_amdgcn_readfirstlane(tid >> 6)];
+#pragma unroll 1
+    for (int tq = 0; tq < 2; ++tq) {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int t = 4 * tq + tt;
+        const int cA = 3 * t, sA = (3 * tt) % 4;   // 12 chunks per tq: the slots are static
+        // ---- phase A: RZ1^T slice t ----
+        arrive(sA);
+        float hv[16], cb[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hv[r] = hn[r];
+        if (t < 7) hload(r0, t + 1, hn);
+        else if (more) hload(r0n, 0, hn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 cc =
+              __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, 16 * h, (32 * t + 8 * j) * 4, 0));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cb[4 * j + i] = cc[i];
+        }
+        ahead(cA, sA, more);
+        const cu32x4* S = slot(sA);
+        f32x16 accA = f32x16{};
+        // fragments one k-step ahead of the MFMAs (sched barriers keep the compiler from hoisting them all)
+        f16x8 fa[2][2];
+        auto lda = [&](int ks, f16x8 (&f)[2]) __attribute__((always_inline)) {
+          const int au = s * 16 + ((2 * ks + h) ^ (s & 15));
+          f[0] = __builtin_bit_cast(f16x8, S[au]);
+          f[1] = __builtin_bit_cast(f16x8, S[512 + au]);
+        };
+        lda(0, fa[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS0; ++ks) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 1 < KS0) lda(ks + 1, fa[(ks + 1) & 1]);
+          accA = rf_mfma3(fa[ks & 1][0], fa[ks & 1][1], xt[ks][0], xt[ks][1], accA);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- epilogue: RH1 slice t (stored), its wave max -> the phase-B product exponent ----
+        float rh[16];
+        float mt = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          rh[r] = one_minus_sq(hv[r]) * (accA[r] * uA + cb[r]);
+          mt = fmaxf(mt, fabsf(rh[r]));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(cu32x4, f32x4{rh[4 * j], rh[4 * j + 1], rh[4 * j + 2], rh[4 * j + 3]}), rrh, hlane,
+              (32 * t + 8 * j) * 4, 0);
+        mR = fmaxf(mR, mt);
+        mt = xmax_f<true>(mt);   // the state's max over the slice (lanes s and s + 32)
+        const int Pt = min(mt > 0.0f ? f16_scale_exp(mt) + eW : 1000, f16_scale_exp(1.0f) + eV);
+        if (t == 0) {
+          Ps = Pt;
+        } else if (__builtin_amdgcn_ballot_w64(Pt < Ps) != 0) {
+          // rare: a state whose slice is larger than all its earlier ones; its accumulator rows step down by an
+          // exact power of two (the other states' by 2^0)
+          if (h == 0) px[s] = Pt < Ps ? Pt - Ps : 0;
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          float f[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) f[r] = __builtin_ldexpf(1.0f, px[8 * (r >> 2) + 4 * h + (r & 3)]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][r] *= f[r];
+          Ps = min(Ps, Pt);
+          __builtin_amdgcn_wave_barrier();
+        }
+        const float sR = __builtin_ldexpf(1.0f, Ps - eW), sH = __builtin_ldexpf(1.0f, Ps - eV);
+        f16x8 aR[2][2], aH[2][2];   // k-step uu: registers 8 uu .. 8 uu + 7 (the permuted k order)
+#pragma unroll
+        for (int uu = 0; uu < 2; ++uu) {
+          rf_split8(rh + 8 * uu, sR, aR[uu][0], aR[uu][1]);
+          rf_split8(hv + 8 * uu, sH, aH[uu][0], aH[uu][1]);
+        }
+        // ---- phase B: RZ2 += RH1_t W1_t + H1_t V1_t, output columns 128 nh .. 128 nh + 127 ----
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh) {
+          const int sB = (3 * tt + 1 + nh) % 4;
+          arrive(sB);
+          if (nh == 1 && t == 7 && more) xload(r0n, xt);   // the next tile's X, ahead of the DMA
+          ahead(cA + 1 + nh, sB, more);
+          const cu32x4* B = slot(sB);
+          // step k = 4 uu + tn; its W / V fragments loaded one step ahead
+          f16x8 fb[2][4];
+          auto ldb = [&](int k, f16x8 (&f)[4]) __attribute__((always_inline)) {
+            const int col = 32 * (k & 3) + s;
+            const int bu = col * 4 + ((2 * (k >> 2) + h) ^ ((col >> 2) & 3));
+            f[0] = __builtin_bit_cast(f16x8, B[bu]);
+            f[1] = __builtin_bit_cast(f16x8, B[512 + bu]);
+            f[2] = __builtin_bit_cast(f16x8, B[1024 + bu]);
+            f[3] = __builtin_bit_cast(f16x8, B[1536 + bu]);
+          };
+          ldb(0, fb[0]);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (k + 1 < 8) ldb(k + 1, fb[(k + 1) & 1]);
+            const int uu = k >> 2, tn = k & 3;
+            const f16x8(&f)[4] = fb[k & 1];
+            f32x16 c = acc[4 * nh + tn];
+            c = rf_mfma3(aR[uu][0], aR[uu][1], f[0], f[1], c);
+            c = rf_mfma3(aH[uu][0], aH[uu][1], f[2], f[3], c);
+            acc[4 * nh + tn] = c;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // ---- RZ2 = acc 2^-Pacc + c1: lane (column 32 tn + s, states 8 j + 4 h + i) ----
+    if (h == 0) px[s] = Ps;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float un[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) un[r] = __builtin_ldexpf(1.0f, -px[8 * (r >> 2) + 4 * h + (r & 3)]);
+    __builtin_amdgcn_wave_barrier();
+    const __amdgpu_buffer_rsrc_t rz =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.RZ2 + r0 * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
+    const unsigned zlane = (unsigned)(4 * h * kRfLd + s) * 4u;   // lane part: state 4 h, column s
+#pragma unroll
+    for (int tn = 0; tn < 8; ++tn) {
+      const float cn = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv1, 4 * s, 128 * tn, 0));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float o = acc[tn][r] * un[r] + cn;
+        mZ = fmaxf(mZ, fabsf(o));
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rz, zlane,
+                                              ((8 * (r >> 2) + (r & 3)) * kRfLd + 32 * tn) * 4, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup has left the CU
+  amax_commit3<true>(a.am_rh1, mR, a.am_rz2, mZ, nullptr, 0.0f, red);
+}
+
+}  // namespace
+
+bool rfwd01_eligible(int L, const int* w, const int* wp) {
+  return L == 3 && w[0] >= 1 && w[0] <= 128 && w[1] == 256 && w[2] == 256 && wp[1] == 256 && wp[2] == 256;
+}
+
+size_t rfwd01_img_bytes() { return (size_t)kRfChunks * kRfUnits * 16; }
+
+void launch_rfwd01_img(const float* theta, const float* v, int64_t offV0, int64_t offW1, int obs,
+                       const unsigned* am_v0, const unsigned* am_w1, const unsigned* am_v1, uint16_t* img,
+                       const int* skip, hipStream_t s) {
+  hipLaunchKernelGGL(rfwd01_img_kernel, dim3(8 * 2560 / 256), dim3(256), 0, s, theta, v, offV0, offW1, obs, am_v0,
+                     am_w1, am_v1, img, skip);
+}
+
+void launch_rfwd01(const Rfwd01Args& a, int num_cus, hipStream_t s) {
+  if (a.n <= 0) return;
+  if (a.obs < 1 || a.obs > 128 || a.ldh != 256 || a.ldz != 256)
+    throw std::runtime_error("rfwd01: unsupported shape");
+  if ((int64_t)4 * a.x_mpad * 64 >= ((int64_t)1 << 31) || a.x_mpad < (a.n + kRfTile - 1) / kRfTile * kRfTile)
+    throw std::runtime_error("rfwd01: X plane geometry");
+  const int64_t ntiles = (a.n + kRfTile - 1) / kRfTile;
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)num_cus);
+  hipLaunchKernelGGL(rfwd01_kernel<8>, dim3(grid), dim3(kRfWaves * 64), 0, s, a);
+}
+
+}  // namespace trpo

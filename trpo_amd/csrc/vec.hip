@@ -11,7 +11,7 @@
 // rounded to float32 at the same point; the float64 scalars of the reference's
 // NumPy-1.x promotion rules (shs, lm, expected-improve rate, line-search ratio)
 // stay float64.
-#include "common.h"
+#include "chain_common.h"
 #include "kernels.h"
 
 #include <stdexcept>
@@ -113,6 +113,212 @@ reduce_slab_kernel(const float* slab, int S, int64_t stride, int64_t P, float* o
     }
     if (blockIdx.x == 0)
       for (int i = (int)gridDim.x + threadIdx.x; i < kRedBlocks; i += blockDim.x) partials[i] = 0.0;
+  }
+}
+
+// The whole CG iteration after the one-launch FVP (single rank, cg_fuse_reduce = 2), in one launch: every block runs
+// reduce_slab_kernel<true> on its 64 parameters (Hv, z = Hv + damping p, its p.z partial), then takes a ticket; the
+// block that arrives last runs cg_xr_kernel's and cg_p_kernel's arithmetic over all P (utils.py:192-200) and, on the
+// fused16 path, builds the next FVP's V images from the new p (fused16_img_kernel's values and exponents), which
+// removes three launches per iteration (cg_xr, cg_p, the image build).  The last block replays the 256-thread blocks
+// of those kernels wave by wave: each of its waves sums the 64 values one of their waves held with the same
+// butterfly, and the virtual blocks' partials and the final sums are added in the same order, so x, r, p, alpha, mu
+// and rdotr are bit-identical to cg_fuse_reduce = 1.  Hand-off: plain stores, s_waitcnt vmcnt(0), workgroup barrier,
+// lane-0 agent release fence, vmcnt(0), agent-scope ticket add; the last arriver's agent acquire fence, vmcnt(0) and
+// a workgroup barrier before its loads (MI355X_MICROARCH.md, inter-workgroup visibility).  It resets the ticket.
+constexpr int kCgStepMax = kRedBlocks * kRsCols;        // P limit: the fixed partial layout (cg_fused_reduce_ok)
+constexpr int kCgStepPer = kCgStepMax / (kRsCols * kRsGroups);   // parameters per thread of the last block (16)
+static_assert(kRsCols * kRsGroups == 1024 && kRedThreads == 256, "cg_step: 16 waves replay 4-wave blocks");
+
+typedef __fp16 fp16x2_t __attribute__((ext_vector_type(2)));
+
+__global__ void __launch_bounds__(kRsCols* kRsGroups)
+cg_step_slabs_kernel(const CgStepArgs a, const ChainImgArgs img, int* img_e) {
+  __shared__ float red[kRsGroups][kRsCols + 1];
+  __shared__ double ws[kRedBlocks], pb[kRedBlocks], w4[4];
+  __shared__ float pl[kCgStepMax];
+  __shared__ unsigned jm[kMaxChainJobs];
+  __shared__ int last;
+  const int it = a.it;
+  if (a.fl->done[it]) {   // converged: this iteration is a no-op, and so is every later one (cg_p_kernel)
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.fl->done[it + 1] = 1;
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t P = a.P;
+  {   // reduce_slab_kernel<true>'s body
+    const int c = tid % kRsCols, g = tid / kRsCols;
+    const int64_t p = (int64_t)blockIdx.x * kRsCols + c;
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    if (p < P) {
+      constexpr int G = kRsGroups;
+      int s = g;
+      for (; s + 3 * G < a.S; s += 4 * G) {
+        a0 += a.slab[(int64_t)s * a.stride + p];
+        a1 += a.slab[(int64_t)(s + G) * a.stride + p];
+        a2 += a.slab[(int64_t)(s + 2 * G) * a.stride + p];
+        a3 += a.slab[(int64_t)(s + 3 * G) * a.stride + p];
+      }
+      for (; s < a.S; s += G) a0 += a.slab[(int64_t)s * a.stride + p];
+    }
+    red[g][c] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (g == 0) {
+      double v = 0.0;
+      if (p < P) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kRsGroups; ++i) acc += red[i][c];
+        a.hv[p] = acc;
+        const float damp = a.sc->damping, pi = a.p[p];
+        const float zi = damp != 0.0f ? acc + damp * pi : acc;
+        a.z[p] = zi;
+        v = (double)pi * (double)zi;
+      }
+      v = wave_sum_d_fast(v);
+      if (c == 0) a.partials[blockIdx.x] = v;
+    }
+  }
+  // ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int is_last = old + 1 == gridDim.x;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = is_last;
+  }
+  __syncthreads();
+  if (!last) return;
+
+  // pz: cg_xr_kernel's sum_partials(partials, kRedBlocks) on a 256-thread block (blocks past the grid: 0)
+  const int nb = (int)gridDim.x;
+  if (wv < 4) {
+    const double v = wave_sum_d_fast(0.0 + (tid < nb ? a.partials[tid] : 0.0));
+    if (lane == 0) w4[wv] = v;
+  }
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < 4; ++w) t += w4[w];
+  const float pz = (float)t;
+  const float rdotr = a.sc->rdotr[it & 1];
+  const float alpha = rdotr / pz;
+  // x += alpha p ; r -= alpha z ; r.r per virtual wave (element i: virtual wave i / 64, lane i % 64)
+  // every load first: x, r, p, z may alias as far as the compiler knows, so a load behind a store would wait for it
+  float rv[kCgStepPer], pv[kCgStepPer], xv[kCgStepPer], zv[kCgStepPer];
+#pragma unroll
+  for (int k = 0; k < kCgStepPer; ++k) {
+    const int64_t i = tid + (int64_t)1024 * k;
+    const bool in = i < P;
+    pv[k] = in ? a.p[i] : 0.0f;
+    xv[k] = in ? a.x[i] : 0.0f;
+    rv[k] = in ? a.r[i] : 0.0f;
+    zv[k] = in ? a.z[i] : 0.0f;
+  }
+  double vv[kCgStepPer];
+#pragma unroll
+  for (int k = 0; k < kCgStepPer; ++k) {
+    const int64_t i = tid + (int64_t)1024 * k;
+    double v = 0.0;
+    if (i < P) {
+      a.x[i] = xv[k] + alpha * pv[k];
+      const float ri = rv[k] - alpha * zv[k];
+      a.r[i] = ri;
+      rv[k] = ri;
+      v += (double)ri * (double)ri;
+    }
+    vv[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < kCgStepPer; ++k) vv[k] = wave_sum_d_fast(vv[k]);   // 16 independent butterflies
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < kCgStepPer; ++k) ws[16 * k + wv] = vv[k];
+  }
+  __syncthreads();
+  if (tid < kRedBlocks) {   // virtual block tid's partial (block_sum_d: its 4 wave sums in order; past P: 0)
+    double s = 0.0;
+    if (tid < kCgStepMax / kRedThreads)
+      for (int w = 0; w < 4; ++w) s += ws[4 * tid + w];
+    pb[tid] = s;
+  }
+  __syncthreads();
+  if (wv < 4) {   // cg_p_kernel's sum_partials(partials2, kRedBlocks)
+    const double v = wave_sum_d_fast(0.0 + pb[tid]);
+    if (lane == 0) w4[wv] = v;
+  }
+  if (tid < kMaxChainJobs) jm[tid] = 0u;
+  __syncthreads();
+  t = 0.0;
+  for (int w = 0; w < 4; ++w) t += w4[w];
+  const float newrdotr = (float)t;
+  const float mu = newrdotr / rdotr;
+  // p = r + mu p, kept in LDS for the image
+#pragma unroll
+  for (int k = 0; k < kCgStepPer; ++k) {
+    const int64_t i = tid + (int64_t)1024 * k;
+    if (i < P) {
+      const float pn = rv[k] + mu * pv[k];
+      a.p[i] = pn;
+      pl[i] = pn;
+    }
+  }
+  if (tid == 0) {
+    a.sc->alpha = alpha;
+    a.sc->mu = mu;
+    a.sc->rdotr[(it + 1) & 1] = newrdotr;
+    a.sc->iters = it + 1;
+    a.fl->done[it + 1] = (newrdotr < a.sc->tol) ? 1 : 0;
+  }
+  if (img.n == 0) return;
+  __syncthreads();
+  for (int j = 0; j < img.n; ++j) {   // the V jobs' max |p| (fused16_img_kernel: over the whole K x O source)
+    const ChainImgJob& jb = img.job[j];
+    if (jb.which != 1) continue;
+    float m = 0.0f;
+    for (int e = tid; e < jb.K * jb.O; e += 1024) m = fmaxf(m, fabsf(pl[jb.src_off + e]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if (lane == 0 && m > 0.0f) atomicMax(&jm[j], __float_as_uint(m));
+  }
+  __syncthreads();
+  // the next FVP's V images (fused16_img_kernel: 8 values per unit, scaled by 2^e, split hi / lo, 16-B stores)
+  for (int j = 0; j < img.n; ++j) {
+    const ChainImgJob& jb = img.job[j];
+    if (jb.which != 1) continue;
+    const int e = f16_scale_exp(__uint_as_float(jm[j]));
+    if (tid == 0) img_e[j] = e;
+    const float sc = __builtin_ldexpf(1.0f, e);
+    const float* src = pl + jb.src_off;
+    const int units = jb.kc * jb.otp * 4;
+    for (int idx = tid; idx < units; idx += 1024) {
+      const int gg = idx & 3, o = (idx >> 2) % jb.otp, c = (idx >> 2) / jb.otp;
+      float x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = 32 * c + chain_perm(8 * gg + q);
+        const bool in = o < jb.O && k < jb.K;
+        x[q] = in ? src[jb.trans ? o * jb.ldw + k : k * jb.ldw + o] * sc : 0.0f;
+      }
+      cu32x4 H, L;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // fused16.hip split2.  (Routing hi through the cu32x4 and back by bit_cast
+        // made hipcc subtract pair 0's hi from every pair: kept in fp16x2 registers here)
+        const fp16x2_t hp = __builtin_amdgcn_cvt_pkrtz(x[2 * q], x[2 * q + 1]);
+        const fp16x2_t lp = __builtin_amdgcn_cvt_pkrtz(x[2 * q] - (float)hp[0], x[2 * q + 1] - (float)hp[1]);
+        H[q] = __builtin_bit_cast(unsigned, hp);
+        L[q] = __builtin_bit_cast(unsigned, lp);
+      }
+      unsigned short* dst = img.img + jb.dst_off + (size_t)c * 2 * jb.otp * 32 + o * 32 + ((gg ^ chain_hsw(o)) << 3);
+      *reinterpret_cast<cu32x4*>(dst) = H;
+      *reinterpret_cast<cu32x4*>(dst + (size_t)jb.otp * 32) = L;
+    }
   }
 }
 
@@ -443,6 +649,19 @@ void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, f
                      partials, partials2, it, skip);
   hipLaunchKernelGGL((cg_p_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, r, p, n, sc,
                      partials2, fl, it);
+}
+
+void launch_cg_step_slabs(const CgStepArgs& a, const ChainImgArgs* img, int* img_e, hipStream_t s) {
+  if (!cg_fused_reduce_ok(a.P)) throw std::runtime_error("cg_step_slabs: too many parameters for one partials row");
+  ChainImgArgs none{};
+  const ChainImgArgs& ia = img ? *img : none;
+  if (img) {   // the V jobs' sources must sit inside P (the last block gathers them from its LDS copy of p)
+    for (int j = 0; j < ia.n; ++j)
+      if (ia.job[j].which == 1 && ia.job[j].src_off + (int64_t)ia.job[j].K * ia.job[j].O > a.P)
+        throw std::runtime_error("cg_step_slabs: image job outside the parameter vector");
+  }
+  hipLaunchKernelGGL(cg_step_slabs_kernel, dim3((unsigned)((a.P + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups), 0,
+                     s, a, ia, img_e);
 }
 
 void launch_dot_partials(const float* a, const float* b, int64_t n, double* partials,
