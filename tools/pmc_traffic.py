@@ -25,6 +25,7 @@ import sys
 SPECS = {
     "fvp_rfwd_l0": ("rowgemm_pl_kernel<1, 1>", 1, 0),                       # X planes, kRHidden (plane.hip)
     "fvp_rfwd_l1": ("rowgemm3_kernel<4, 2, 2, 4, 11, 2, 1, 2, 32>", 1, 0),  # kRZ into the tail (BK 32)
+    "fvp_rfwd01": ("rfwd01_kernel<8>", 1, 0),                               # layers 0 + 1 R-forward (rfwd.hip)
     "fvp_rbwdwg_l1": ("rbwd0_kernel<2>", 1, 0),                             # R-backward + X^T RD_0 (rbwd0.hip)
     "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
     # C2 / C3: the one-launch FVP (fused16.hip mode 0; every substring must be in the name)

@@ -9,18 +9,23 @@
 // is not read back, and H1 is read once.  Bytes per state: X's f16 planes 512 + H1 1024 + RH1 1024 + RZ2 1024 =
 // 3584 (the two launches: 5632).
 //
-// Layout: one workgroup of 8 waves per CU (persistent over 256-state tiles); wave w owns 32 states of the tile
-// and all 256 output columns (128 accumulator registers).  For each 32-feature slice t of layer 1:
+// Layout: one workgroup of 4 waves per CU (persistent over 128-state tiles, 512 registers per wave: the 128
+// accumulators in AGPRs, X of the wave's states in VGPRs for the whole tile); wave w owns 32 states of the tile
+// and all 256 output columns.  For each 32-feature slice t of layer 1:
 //  * phase A: RZ1^T[32 features x 32 states] = V0^T X^T on v_mfma_f32_32x32x16_f16 (V0^T from LDS as the A
-//    operand, X's pre-split f16 planes from HBM / L2 as the B operand), 3 products;
+//    operand, X's pre-split f16 planes as the B operand, loaded once per tile), 3 products;
 //  * epilogue: the accumulator lane holds one state and features 8j + 4h + i (j, i = 0..3, h = lane / 32): RH1
 //    and H1 in that layout are exactly the A operand of the next product with its k order permuted (k-step u
 //    takes registers 8u..8u+7), so RH1 never leaves registers on its way to the second GEMM;
 //  * phase B: RZ2[32 states x 256] += RH1_t W1_t + H1_t V1_t (W1 / V1 rows of slice t, k-permuted the same way,
 //    from LDS as B operands), 3 products per segment.
-// Weights stream through a 4-slot LDS ring by LDS-DMA (24 chunks per tile: V0^T slice t 16 KB, then W1 / V1
-// rows of slice t for output columns 0-127 and 128-255, 32 KB each), built once per FVP in that order by
-// rfwd01_img_kernel (pre-swizzled: the DMA is a straight copy).  Each chunk is DMA'd three chunks ahead.
+// Weights and H1 stream through a 4-slot LDS ring by LDS-DMA (24 chunks per tile: V0^T slice t + H1 slice t, then
+// W1 / V1 rows of slice t for output columns 0-127 and 128-255, 32 KB each; the weight chunks from an image built
+// once per FVP in that order by rfwd01_img_kernel, pre-swizzled, so the DMA is a straight copy), each DMA'd three
+// chunks ahead; no other loads in the loop but X once per tile, so the DMA waits are counted exactly (arrive()).
+// Measured (profiles/r6o): 10.46 ms at C4 against 3.93 + 7.99 for the two launches; ablations: without the
+// phase-B MFMAs 6.6 ms, without any MFMA 6.0: the 5 KB per state of weights the 128-state tiles re-stream by DMA
+// (50 GB per FVP with H1, ~8 TB/s) bound the launch, and the MFMAs do not hide under it.
 //
 // Scales (f16 hi + lo split, kernels.h f16_scale_exp): X from its plane exponent, V0 / W1 / V1 from their
 // running-max slots; RH1 (made in the launch) per state and slice from the state's max |RH1_t| (an A-operand row
@@ -36,6 +41,17 @@ namespace trpo {
 namespace {
 
 typedef __fp16 rf_h2 __attribute__((ext_vector_type(2)));
+
+#ifndef RF_SGB
+#define RF_SGB 1   // 1: each k-step region issues its next fragments' LDS reads before its MFMAs (sched_group_barrier)
+#endif
+#ifndef RF_PAIR
+#define RF_PAIR 0  // 1: phase B steps in pairs of output tiles, the two accumulator chains interleaved
+#endif
+#ifndef RF_ABL
+#define RF_ABL 0   // timing ablations only (tools/variant.sh), bits: 1 = no phase-B MFMAs, 2 = no phase-B LDS reads,
+                   // 4 = no weight DMA, 8 = no RH1 / RZ2 stores, 16 = no H1 / X loads, 32 = no phase-A MFMAs
+#endif
 
 constexpr int kRfUnits = 2048;                 // 16-B units of a ring slot / image chunk (32 KB)
 constexpr int kRfChunks = 24;                  // chunks per tile
@@ -114,13 +130,30 @@ __global__ void __launch_bounds__(256) rfwd01_img_kernel(const float* __restrict
   dst[plane_units] = __builtin_bit_cast(cu32x4, lo);
 }
 
+// One LDS-DMA instruction (buffer_load_dwordx4 ... lds): 16 B per lane from the buffer at voff + soff into LDS at the
+// wave-uniform byte address lds + 16 * lane (soff is added to the lane offset: an soffset operand must be an SGPR,
+// and a constant one would reach the assembler as a literal).  Inline asm, opaque to hipcc's s_waitcnt bookkeeping: the kernel counts
+// the completions itself (arrive()).  M0 is saved and restored around it (the compiler owns M0).
+__device__ __forceinline__ void rf_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff + soff), "s"(rsrc), "s"(lds));
+}
+
 template <int KS0>   // 16-deep k-steps over obs (obs <= 16 KS0)
 __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Args a) {
-  __shared__ cu32x4 q0[kRfUnits], q1[kRfUnits], q2[kRfUnits], q3[kRfUnits];   // the ring: chunk c in slot c % 4
+  // the ring: chunk c in slot c % 4.  An A chunk holds V0^T slice t (image units 0..1023) and H1 slice t of the
+  // tile's 128 states (units 1024..2047, 256 per wave: row r, column unit cu at r * 8 + (cu ^ ((r >> 1) & 7)), so the
+  // epilogue's reads of one column unit over 16 rows hit 16 distinct bank slots); a B chunk the W1 / V1 rows.
+  __shared__ cu32x4 q0[kRfUnits], q1[kRfUnits], q2[kRfUnits], q3[kRfUnits];
+  __shared__ float cvec[2][256];      // the tangent biases c0, c1
   __shared__ float red[3][16];
   __shared__ int pex[kRfWaves][32];   // per-state exponents, from the A-operand lanes to the accumulator lanes
   if (a.skip && *a.skip) return;
   const int tid = threadIdx.x, lane = tid & 63, s = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int eX = __builtin_amdgcn_readfirstlane(*a.eX);
   const int eV0 = __builtin_amdgcn_readfirstlane(amax_exp(a.am_v0));
   const int eW = __builtin_amdgcn_readfirstlane(amax_exp(a.am_w1));
@@ -131,39 +164,62 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
       __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, kRfChunks * kRfUnits * 16, 0x00020000);
   const __amdgpu_buffer_rsrc_t rxh = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xh, 0, 0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rxl = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xl, 0, 0x7ffffff0, 0x00020000);
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Ordering rule: vector-memory returns retire in issue order, so a wait for an ordinary load also waits for every
-  // DMA issued before it.  Each chunk therefore issues its ordinary loads (the next X / H1, c0) BEFORE its DMA, and
-  // the DMA three chunks ahead never stands in front of a load the current chunk consumes.
+  for (int i = tid; i < 256; i += kRfWaves * 64) {
+    cvec[0][i] = a.c0[i];
+    cvec[1][i] = a.c1[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // ordinary loads retired before the first DMA
   auto slot = [&](int k) -> cu32x4* { return k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3; };
-  // chunk c (0..23) of the image into slot sl (= c % 4): 1 KB per wave-instruction, lane-linear
-  auto dma = [&](int c, int sl) __attribute__((always_inline)) {
-    const int units = c % 3 == 0 ? 1024 : 2048;
+  auto rows_of = [&](int64_t r0w) { return (int)(a.n - r0w < 32 ? (a.n - r0w > 0 ? a.n - r0w : 0) : 32); };
+  // chunk c (0..23) into slot sl (= c % 4), 8 DMA instructions per wave: a B chunk from the image; an A chunk half
+  // from the image, half this wave's 32 H1 rows of slice t = c / 3 (r0w: the wave's first state of the chunk's tile;
+  // rows past n land as zeros)
+  auto dma = [&](int c, int sl, int64_t r0w) __attribute__((always_inline)) {
+    if constexpr ((RF_ABL & 4) != 0) return;
+    const unsigned lds0 = (unsigned)(uintptr_t)slot(sl);
+    const bool A = c % 3 == 0;
 #pragma unroll
-    for (int i = 0; i < 2048 / (kRfWaves * 64); ++i) {
-      const int base = wv * 64 + i * kRfWaves * 64;
-      if (base < units)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rimg, (__attribute__((address_space(3))) void*)(slot(sl) + base),
-                                                 16, (base + lane) * 16, c * kRfUnits * 16, 0, 0);
+    for (int i = 0; i < (A ? 4 : 8); ++i) {
+      const int base = wv * 64 + i * kRfWaves * 64;   // units
+      rf_dma16(rimg, (unsigned)(base + lane) * 16u, (unsigned)c * kRfUnits * 16u, lds0 + (unsigned)base * 16u);
+    }
+    if (A) {
+      const int t = c / 3;
+      const __amdgpu_buffer_rsrc_t rh =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.H1 + r0w * kRfLd), 0, rows_of(r0w) * kRfLd * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 8 * i + (lane >> 3), cu = (lane & 7) ^ ((r >> 1) & 7);
+        rf_dma16(rh, (unsigned)(r * kRfLd + 4 * cu) * 4u, (unsigned)(32 * t) * 4u,
+                 lds0 + (unsigned)(1024 + wv * 256 + 64 * i) * 16u);
+      }
     }
   };
-  // this wave's DMA into slot sl has landed (the compiler's wait before the probe read), then every wave's
-  // (barrier: the chunk is visible, and every wave is past the previous chunk, whose slot is the next DMA's)
-  auto arrive = [&](int sl) __attribute__((always_inline)) {
+  // Begin chunk c: this wave's DMA into the chunk's slot has landed, then every wave's (the barrier: the chunk is
+  // visible, and every wave is past chunk c - 1, whose slot takes chunk c + 3's DMA next).  Completions retire in
+  // issue order; behind chunk c's 8 DMA instructions this wave has issued at least those of chunks c + 1 and c + 2
+  // (16) -- more VMEM operations only where it also issued loads / stores after them -- so vmcnt(16) is a
+  // sufficient wait (first tile's A_0: exactly 16 behind it).  Across a tile boundary more than 63 operations sit
+  // behind (the RZ2 stores): vmcnt(63) there.
+  auto arrive = [&](bool far) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
-    const cu32x4 probe = slot(sl)[tid];
-    asm volatile("" ::"v"(probe));
+    if (far) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     lds_barrier();
-  };
-  // the DMA three chunks after chunk c (c + 3 < 24: this tile's; else the next tile's, if this workgroup has one)
-  auto ahead = [&](int c, int sl, bool more) __attribute__((always_inline)) {
-    if (c + 3 < kRfChunks) dma(c + 3, (sl + 3) % 4);
-    else if (more) dma(c + 3 - kRfChunks, (sl + 3) % 4);
   };
   // X's f16 planes, all k-steps, of one state (B operand: lane (state s, half h) holds obs 16 ks + 8 h .. + 7)
   // (row0 = the wave's first state: uniform, so every load is one lane offset + one scalar offset)
   const unsigned xlane = (unsigned)(s * 32 + 8 * h) * 2u;
   auto xload = [&](int64_t row0, f16x8 (&x)[KS0][2]) __attribute__((always_inline)) {
+    if constexpr ((RF_ABL & 16) != 0) {
+#pragma unroll
+      for (int ks = 0; ks < KS0; ++ks) {
+        unsigned u = (unsigned)row0 + ks;
+        asm volatile("" : "+v"(u));
+        x[ks][0] = x[ks][1] = __builtin_bit_cast(f16x8, cu32x4{u, u, u, u});
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS0; ++ks) {
       const int so = (int)((((unsigned)(ks >> 1) * (unsigned)a.x_mpad + (unsigned)row0) * 32u + 16u * (ks & 1)) * 2u);
@@ -171,39 +227,23 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
       x[ks][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rxl, xlane, so, 0));
     }
   };
-  const unsigned hlane = (unsigned)(s * kRfLd + 4 * h) * 4u;   // H1 / RH1 rows: lane part of the offset
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)a.c0, 0, 256 * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.c1, 0, 256 * 4, 0x00020000);
-  // H1's slice t of one wave's 32 states (rows past n read 0)
-  auto hload = [&](int64_t r0w, int t, float (&hv)[16]) __attribute__((always_inline)) {
-    const int rows = (int)(a.n - r0w < 32 ? (a.n - r0w > 0 ? a.n - r0w : 0) : 32);
-    const __amdgpu_buffer_rsrc_t rh =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.H1 + r0w * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 v4 =
-          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, hlane, (32 * t + 8 * j) * 4, 0));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hv[4 * j + i] = v4[i];
-    }
-  };
+  const unsigned hlane = (unsigned)(s * kRfLd + 4 * h) * 4u;   // RH1 rows: lane part of the offset
 
   f16x8 xt[KS0][2];   // X of this wave's 32 states, the whole tile
-  float hn[16];       // H1 of the next slice, loaded one slice ahead
-  if ((int64_t)blockIdx.x < ntiles) {
-    xload((int64_t)blockIdx.x * kRfTile + wv * 32, xt);
-    hload((int64_t)blockIdx.x * kRfTile + wv * 32, 0, hn);
+  xload((int64_t)blockIdx.x * kRfTile + wv * 32, xt);   // (grid <= tiles: a real tile)
+  {
+    const int64_t r0f = (int64_t)blockIdx.x * kRfTile + wv * 32;
+    dma(0, 0, r0f);
+    dma(1, 1, r0f);
+    dma(2, 2, r0f);
   }
-  dma(0, 0);
-  dma(1, 1);
-  dma(2, 2);
 
   float mR = 0.0f, mZ = 0.0f;   // running max |RH1|, |RZ2| of this lane
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool more = tile + gridDim.x < ntiles;
+    const bool first = tile == (int64_t)blockIdx.x;
     const int64_t r0 = tile * kRfTile + wv * 32;   // this wave's first state (wave-uniform: the buffer bases)
     const int64_t r0n = r0 + (int64_t)gridDim.x * kRfTile;     // ... in the next tile
-    const int rows = (int)(a.n - r0 < 32 ? (a.n - r0 > 0 ? a.n - r0 : 0) : 32);
+    const int rows = rows_of(r0);
     const __amdgpu_buffer_rsrc_t rrh =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.RH1 + r0 * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
     f32x16 acc[8];
@@ -211,28 +251,17 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
     for (int i = 0; i < 8; ++i) acc[i] = f32x16{};
     int Ps = 0;   // this lane's state's product exponent (set by slice 0, lowered when a later slice needs it)
     // accumulator register r of this lane holds state 8 (r >> 2) + 4 h + (r & 3): its exponent comes through LDS
-    int* px = pex[__builtin_amdgcn_readfirstlane(tid >> 6)];
+    int* px = pex[wv];
 #pragma unroll 1
     for (int tq = 0; tq < 2; ++tq) {
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const int t = 4 * tq + tt;
         const int cA = 3 * t, sA = (3 * tt) % 4;   // 12 chunks per tq: the slots are static
+        const bool far = t == 0 && !first;
         // ---- phase A: RZ1^T slice t ----
-        arrive(sA);
-        float hv[16], cb[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) hv[r] = hn[r];
-        if (t < 7) hload(r0, t + 1, hn);
-        else if (more) hload(r0n, 0, hn);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 cc =
-              __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, 16 * h, (32 * t + 8 * j) * 4, 0));
-#pragma unroll
-          for (int i = 0; i < 4; ++i) cb[4 * j + i] = cc[i];
-        }
-        ahead(cA, sA, more);
+        arrive(far);
+        dma(cA + 3 < kRfChunks ? cA + 3 : cA + 3 - kRfChunks, (sA + 3) % 4, cA + 3 < kRfChunks ? r0 : r0n);
         const cu32x4* S = slot(sA);
         f32x16 accA = f32x16{};
         // fragments one k-step ahead of the MFMAs (sched barriers keep the compiler from hoisting them all)
@@ -247,19 +276,31 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         for (int ks = 0; ks < KS0; ++ks) {
           __builtin_amdgcn_sched_barrier(0);
           if (ks + 1 < KS0) lda(ks + 1, fa[(ks + 1) & 1]);
-          accA = rf_mfma3(fa[ks & 1][0], fa[ks & 1][1], xt[ks][0], xt[ks][1], accA);
+          if constexpr ((RF_ABL & 32) == 0) accA = rf_mfma3(fa[ks & 1][0], fa[ks & 1][1], xt[ks][0], xt[ks][1], accA);
+          if (RF_SGB && ks + 1 < KS0) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
-        // ---- epilogue: RH1 slice t (stored), its wave max -> the phase-B product exponent ----
-        float rh[16];
+        // ---- epilogue: RH1 slice t (stored), the state's max -> its phase-B product exponent ----
+        float hv[16], rh[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cu = 2 * j + h;
+          const f32x4 v4 = __builtin_bit_cast(f32x4, S[1024 + wv * 256 + s * 8 + (cu ^ ((s >> 1) & 7))]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hv[4 * j + i] = v4[i];
+        }
         float mt = 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          rh[r] = one_minus_sq(hv[r]) * (accA[r] * uA + cb[r]);
+          const float cb = cvec[0][32 * t + 8 * (r >> 2) + 4 * h + (r & 3)];
+          rh[r] = one_minus_sq(hv[r]) * (accA[r] * uA + cb);
           mt = fmaxf(mt, fabsf(rh[r]));
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4 && (RF_ABL & 8) == 0; ++j)
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(cu32x4, f32x4{rh[4 * j], rh[4 * j + 1], rh[4 * j + 2], rh[4 * j + 3]}), rrh, hlane,
               (32 * t + 8 * j) * 4, 0);
@@ -294,10 +335,10 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         // ---- phase B: RZ2 += RH1_t W1_t + H1_t V1_t, output columns 128 nh .. 128 nh + 127 ----
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
-          const int sB = (3 * tt + 1 + nh) % 4;
-          arrive(sB);
-          if (nh == 1 && t == 7 && more) xload(r0n, xt);   // the next tile's X, ahead of the DMA
-          ahead(cA + 1 + nh, sB, more);
+          const int cB = cA + 1 + nh, sB = (3 * tt + 1 + nh) % 4;
+          arrive(far);
+          if (nh == 1 && t == 7) xload(r0n < a.x_mpad ? r0n : 0, xt);   // the next tile's X (none: any valid rows)
+          dma(cB + 3 < kRfChunks ? cB + 3 : cB + 3 - kRfChunks, (sB + 3) % 4, cB + 3 < kRfChunks ? r0 : r0n);
           const cu32x4* B = slot(sB);
           // step k = 4 uu + tn; its W / V fragments loaded one step ahead
           f16x8 fb[2][4];
@@ -313,19 +354,25 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             __builtin_amdgcn_sched_barrier(0);
-            if (k + 1 < 8) ldb(k + 1, fb[(k + 1) & 1]);
+            if (k + 1 < 8 && (RF_ABL & 2) == 0) ldb(k + 1, fb[(k + 1) & 1]);
             const int uu = k >> 2, tn = k & 3;
             const f16x8(&f)[4] = fb[k & 1];
-            f32x16 c = acc[4 * nh + tn];
-            c = rf_mfma3(aR[uu][0], aR[uu][1], f[0], f[1], c);
-            c = rf_mfma3(aH[uu][0], aH[uu][1], f[2], f[3], c);
-            acc[4 * nh + tn] = c;
+            if ((RF_ABL & 1) == 0) {
+              f32x16 c = acc[4 * nh + tn];
+              c = rf_mfma3(aR[uu][0], aR[uu][1], f[0], f[1], c);
+              c = rf_mfma3(aH[uu][0], aH[uu][1], f[2], f[3], c);
+              acc[4 * nh + tn] = c;
+            }
+            if (RF_SGB && (RF_ABL & 3) == 0 && k + 1 < 8) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
-    // ---- RZ2 = acc 2^-Pacc + c1: lane (column 32 tn + s, states 8 j + 4 h + i) ----
+    // ---- RZ2 = acc 2^-P + c1: lane (column 32 tn + s, states 8 j + 4 h + i) ----
     if (h == 0) px[s] = Ps;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -338,13 +385,14 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
     const unsigned zlane = (unsigned)(4 * h * kRfLd + s) * 4u;   // lane part: state 4 h, column s
 #pragma unroll
     for (int tn = 0; tn < 8; ++tn) {
-      const float cn = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv1, 4 * s, 128 * tn, 0));
+      const float cn = cvec[1][32 * tn + s];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float o = acc[tn][r] * un[r] + cn;
         mZ = fmaxf(mZ, fabsf(o));
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rz, zlane,
-                                              ((8 * (r >> 2) + (r & 3)) * kRfLd + 32 * tn) * 4, 0);
+        if constexpr ((RF_ABL & 8) == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rz, zlane,
+                                                ((8 * (r >> 2) + (r & 3)) * kRfLd + 32 * tn) * 4, 0);
       }
     }
   }
