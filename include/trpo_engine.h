@@ -225,6 +225,8 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * (x, r, p, the next FVP's f16 V image) runs in the same launch, in the workgroup that finishes last,
  * bit-identical to 1 but slower (one CU's serial tail); 0 = off: 0 and 1 group the p.z partials differently, so
  * each is deterministic but their CG scalars are not bit-identical to each other).
+ * "cg_p_img" (the fused16 path: each CG iteration's p update and the next FVP's f16 V images in one launch,
+ * bit-identical: 1 = on, the default; 0 = two launches).
  * "rfwd01" (the FVP's R-forward through layers 0 and 1 as one launch, rfwd.hip, where two hidden layers of 256
  * with obs <= 128 run the fused tail: 1 = on, the default; 0 = the plane and row GEMM launches).
  * "ls_fused" = 2 mixes two forwards inside one line search (loss_before from the per-layer forward, the

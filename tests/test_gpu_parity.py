@@ -291,6 +291,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"ls_fused": 2},                                          # per-layer prepare forward, one-launch trial forwards
     {"cg_fuse_reduce": 0},                                    # the CG's separate slab reduction on fused16 shapes
     {"cg_fuse_reduce": 2},                                    # the whole CG iteration after the FVP in one launch
+    {"cg_p_img": 0},                                          # the CG's p update and the V images as two launches
     {"rfwd01": 0},                                            # R-forward of layers 0 / 1 as two launches (C4 dims)
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
@@ -300,7 +301,8 @@ def test_kernel_variants_parity(gpu_available, opts):
     from trpo_amd._lib import get_option, set_option
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
                                            "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
-                                           "splits", "pg_splits", "ls_fused", "cg_fuse_reduce", "rfwd01")}
+                                           "splits", "pg_splits", "ls_fused", "cg_fuse_reduce", "rfwd01",
+                                           "cg_p_img")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -987,27 +989,31 @@ def test_head_bwd2_vs_rowgemm_and_oracle(gpu_available, obs, hidden, A, n):
     assert_vec_close(out[2][0], out[0][0], REL, "f32 MFMA dual vs row-GEMM backward g")
 
 
+@pytest.mark.parametrize("opt,modes", [
+    ("cg_fuse_reduce", (1, 2)),   # 2: x / r / p and the next V image in the slab reduction's launch (last workgroup)
+    ("cg_p_img", (0, 1)),         # 1 (default): the p update and the next V images in one launch (p ping-pongs)
+], ids=lambda v: str(v))
 @pytest.mark.parametrize("obs,hidden,A,n", [
     (11, [64, 64], 3, 50_000),         # C2: the CG step builds the next FVP's V images
     (128, [64, 64], 18, 20_000),       # C3 dims: P = 13,586, 213 reduction blocks
     (4, [64], 2, 1000),                # C1 dims: one hidden layer
     (37, [50, 33], 7, 129),            # padded widths, one FVP workgroup
 ])
-def test_cg_step_one_launch_bitwise(gpu_available, obs, hidden, A, n):
-    """cg_fuse_reduce = 2 (the iteration's x / r / p updates and the next V image in the slab reduction's launch,
-    run by the workgroup that arrives last) is bit-identical to cg_fuse_reduce = 1 (the default, three more launches): the CG
-    solution at residual_tol 0 and with an early exit (utils.py:199-200), and whole updates, eager and replayed
-    from the captured graph."""
+def test_cg_step_one_launch_bitwise(gpu_available, obs, hidden, A, n, opt, modes):
+    """The fused CG-step launches are bit-identical to the separate ones: cg_fuse_reduce = 2 (the iteration's x / r / p
+    updates and the next V image in the slab reduction's launch, run by the workgroup that arrives last) against 1,
+    and cg_p_img = 1 (the p update with the next V images) against 0: the CG solution at residual_tol 0 and with
+    early exits (utils.py:199-200), and whole updates, eager and replayed from the captured graph."""
     from trpo_amd import Engine, UpdateParams
     from trpo_amd._lib import get_option, set_option
     spec = O.PolicySpec(obs, hidden, A)
     dd = O.synthetic_batch(spec, n, seed=31)
     b = np.random.RandomState(32).standard_normal(spec.n_params).astype(np.float32)
-    dflt = get_option("cg_fuse_reduce")
+    dflt = get_option(opt)
     runs = {}
     try:
-        for mode in (1, 2):
-            set_option("cg_fuse_reduce", mode)
+        for mode in modes:
+            set_option(opt, mode)
             e = Engine(obs, hidden, A, max_rows=n)
             e.set_flat(dd["theta"])
             e.set_batch(dd["X"], dd["actions"], dd["advant"].astype(np.float32), dd["old_dist"])
@@ -1025,15 +1031,16 @@ def test_cg_step_one_launch_bitwise(gpu_available, obs, hidden, A, n):
             runs[mode] = out
             e.close()
     finally:
-        set_option("cg_fuse_reduce", dflt)
-    for k, v in runs[1].items():
+        set_option(opt, dflt)
+    m0, m1 = modes
+    for k, v in runs[m0].items():
         if isinstance(v, np.ndarray):
-            assert np.array_equal(v, runs[2][k]), (k, float(np.abs(v - runs[2][k]).max()))
+            assert np.array_equal(v, runs[m1][k]), (k, float(np.abs(v - runs[m1][k]).max()))
         else:
-            assert v == runs[2][k], (k, v, runs[2][k])
+            assert v == runs[m1][k], (k, v, runs[m1][k])
     ref = O.fvp_undamped(dd["theta"].astype(np.float64), dd["X"], b.astype(np.float64), spec)
-    assert np.all(np.isfinite(ref)) and runs[2]["it0"] == 10
-    assert min(runs[2][f"it{f}"] for f in (0.5, 1e-2, 1e-4)) < 10   # an early exit was exercised
+    assert np.all(np.isfinite(ref)) and runs[m1]["it0"] == 10
+    assert min(runs[m1][f"it{f}"] for f in (0.5, 1e-2, 1e-4)) < 10   # an early exit was exercised
 
 
 def _block_slices(spec):

@@ -57,6 +57,7 @@ struct trpo_engine {
   std::vector<void*> allocs;
   float *theta = nullptr, *theta_prev = nullptr, *theta_trial = nullptr, *theta_ls = nullptr;
   float *g = nullptr, *bneg = nullptr, *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr;
+  float* p2 = nullptr;   // the CG's second direction buffer (p ping-pongs when the p update writes a new buffer)
   float *hv = nullptr, *stepdir = nullptr, *fullstep = nullptr, *vin = nullptr, *vout = nullptr;
   std::vector<float*> WF, WB, WFt;   // packed [W;V], [W^T;V^T], trial forward weights
   float* WBt_scratch = nullptr;
@@ -354,7 +355,7 @@ struct trpo_engine {
     }
     cap = max_rows;
 
-    for (float** v : {&theta, &theta_prev, &theta_trial, &theta_ls, &g, &bneg, &x, &r, &p, &z, &hv,
+    for (float** v : {&theta, &theta_prev, &theta_trial, &theta_ls, &g, &bneg, &x, &r, &p, &p2, &z, &hv,
                       &stepdir, &fullstep, &vin, &vout})
       *v = dalloc<float>(P);
     int maxpad = 4;
@@ -1646,21 +1647,29 @@ struct trpo_engine {
     launch_cg_init(b, xo, r, p, P, partA, sc, fl, tol, damping, stream);
     check_launch();
     f16_v_img_ready = false;
+    float* pc = p;    // this iteration's direction; cg_p_img16 writes the next one into the other buffer
+    float* pn = p2;
     for (int it = 0; it < iters; ++it) {
       int slabs = 0;
-      fvp(p, hv, &fl->done[it], g_options.cg_fuse_reduce ? &slabs : nullptr);
+      fvp(pc, hv, &fl->done[it], g_options.cg_fuse_reduce ? &slabs : nullptr);
       Scope sp(this, "cg_vec");
       if (slabs > 0 && g_options.cg_fuse_reduce == 2) {
         // the rest of the iteration in the slab reduction's launch; on the fused16 path it also builds the next
         // iteration's V image, which that FVP then does not launch (fvp_fused16)
-        const CgStepArgs ca{slab, slabs, it, slab_stride, P, hv, xo, r, p, z, sc, partA, fl, cg_ticket};
+        const CgStepArgs ca{slab, slabs, it, slab_stride, P, hv, xo, r, pc, z, sc, partA, fl, cg_ticket};
         const bool img = use_fused16() && it + 1 < iters;
         launch_cg_step_slabs(ca, img ? &f16_jobs : nullptr, f16_e, stream);
         f16_v_img_ready = img;
+      } else if (slabs > 0 && g_options.cg_p_img != 0 && use_fused16() && it + 1 < iters) {
+        // the p update and the next FVP's V images in one launch (the next p in the other buffer)
+        launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, pc, z, P, sc, partA, partB, fl, it, stream, false);
+        launch_cg_p_img16(f16_jobs, r, pc, pn, P, sc, partB, fl, it, f16_e, stream);
+        f16_v_img_ready = true;
+        std::swap(pc, pn);
       } else if (slabs > 0) {
-        launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+        launch_cg_iter_slabs(slab, slabs, slab_stride, hv, xo, r, pc, z, P, sc, partA, partB, fl, it, stream);
       } else {
-        launch_cg_iter(hv, xo, r, p, z, P, sc, partA, partB, fl, it, stream);
+        launch_cg_iter(hv, xo, r, pc, z, P, sc, partA, partB, fl, it, stream);
       }
       check_launch();
     }
@@ -2769,6 +2778,7 @@ static int* option_slot(const std::string& k) {
   if (k == "ls_fused") return &g_options.ls_fused;
   if (k == "cg_fuse_reduce") return &g_options.cg_fuse_reduce;
   if (k == "rfwd01") return &g_options.rfwd01;
+  if (k == "cg_p_img") return &g_options.cg_p_img;
   throw ArgError("unknown option " + k);
 }
 

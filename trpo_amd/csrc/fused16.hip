@@ -173,6 +173,84 @@ __global__ void __launch_bounds__(256) fused16_img_kernel(const ChainImgArgs a, 
   *reinterpret_cast<cu32x4*>(dst + (size_t)j.otp * 32) = L;
 }
 
+// The CG's p update (utils.py:196-198, vec.hip cg_p_kernel) fused with the next FVP's V images (fused16_img_kernel,
+// which = 1) in one launch: p_new = r + mu p_old goes to a second buffer (the image blocks read p_old and r while the
+// writer blocks write p_new), and every image block forms the p_new values of its job itself (the job's max too).
+// blockIdx.y < jobs: image blocks; blockIdx.y == jobs: the writer blocks (grid-stride over P).  mu and the scalars
+// as cg_p_kernel (256-thread blocks, the same fixed-order sum of the r.r partials): bit-identical.
+__global__ void __launch_bounds__(256) cg_p_img16_kernel(const ChainImgArgs a, const float* r, const float* p_old,
+                                                         float* p_new, int64_t n, UpdScalars* sc,
+                                                         const double* partials2, CGFlags* fl, int it, int* img_e) {
+#pragma clang fp contract(off)
+  __shared__ double scratch[kRedThreads / 64];
+  __shared__ float red[4];
+  const bool writer = (int)blockIdx.y == a.n;
+  if (fl->done[it]) {   // converged: a no-op, and so is every later iteration (cg_p_kernel)
+    if (writer && blockIdx.x == 0 && threadIdx.x == 0) fl->done[it + 1] = 1;
+    return;
+  }
+  if (!writer && a.job[blockIdx.y].which != 1) return;
+  const float newrdotr = (float)sum_partials(partials2, kRedBlocks, scratch);
+  const float rdotr = sc->rdotr[it & 1];
+  const float mu = newrdotr / rdotr;
+  if (writer) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+      p_new[i] = r[i] + mu * p_old[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      sc->mu = mu;
+      sc->rdotr[(it + 1) & 1] = newrdotr;
+      sc->iters = it + 1;
+      fl->done[it + 1] = (newrdotr < sc->tol) ? 1 : 0;
+    }
+    return;
+  }
+  const ChainImgJob& j = a.job[blockIdx.y];
+  const float* rs = r + j.src_off;
+  const float* ps = p_old + j.src_off;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const bool live = idx < j.kc * j.otp * 4;
+  const int gg = idx & 3;
+  const int o = (idx >> 2) % j.otp;
+  const int c = (idx >> 2) / j.otp;
+  float x[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = 32 * c + chain_perm(8 * gg + q);
+    const bool in = live && o < j.O && k < j.K;
+    const int e = in ? (j.trans ? o * j.ldw + k : k * j.ldw + o) : 0;
+    const float val = rs[e] + mu * ps[e];
+    x[q] = in ? val : 0.0f;
+  }
+  float m = 0.0f;
+  const int last = j.K * j.O - 1;
+#pragma unroll
+  for (int u = 0; u < kImgMax / 256; ++u) {
+    const int e = min((int)threadIdx.x + 256 * u, last);
+    m = fmaxf(m, fabsf(rs[e] + mu * ps[e]));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = f16_scale_exp(m);
+  if (blockIdx.x == 0 && threadIdx.x == 0) img_e[blockIdx.y] = e;
+  if (!live) return;
+  const float sc2 = __builtin_ldexpf(1.0f, e);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) x[q] *= sc2;
+  cu32x4 H, L;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const cu32x2 pp = split2(x[2 * i], x[2 * i + 1]);
+    H[i] = pp[0];
+    L[i] = pp[1];
+  }
+  unsigned short* dst = a.img + j.dst_off + (size_t)c * 2 * j.otp * 32 + o * 32 + ((gg ^ chain_hsw(o)) << 3);
+  *reinterpret_cast<cu32x4*>(dst) = H;
+  *reinterpret_cast<cu32x4*>(dst + (size_t)j.otp * 32) = L;
+}
+
 // image jobs (kernels.h, kFused16Jobs): NH = 2: V_0 | W_1 V_1 | W_2 V_2 | W_2^T V_2^T | W_1^T V_1^T;
 // NH = 1: V_0 | W_1 V_1 | W_1^T V_1^T
 enum { jV0 = 0, jW1, jV1, jW2, jV2, jW2t, jV2t, jW1t, jV1t };
@@ -1286,6 +1364,20 @@ void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* 
     if (j.which == which) maxb = std::max(maxb, (j.kc * j.otp * 4 + 255) / 256);
   }
   hipLaunchKernelGGL(fused16_img_kernel, dim3(maxb, a.n), dim3(256), 0, s, a, theta, v, which, skip, img_e);
+}
+
+void launch_cg_p_img16(const ChainImgArgs& a, const float* r, const float* p_old, float* p_new, int64_t n,
+                       UpdScalars* sc, const double* partials2, CGFlags* fl, int it, int* img_e, hipStream_t s) {
+  int maxb = 1;
+  for (int i = 0; i < a.n; ++i) {
+    const ChainImgJob& j = a.job[i];
+    if (j.K * j.O > kImgMax || j.K * j.O < 1 || j.src_off + (int64_t)j.K * j.O > n)
+      throw std::runtime_error("cg_p_img16: image job");
+    if (j.which == 1) maxb = std::max(maxb, (j.kc * j.otp * 4 + 255) / 256);
+  }
+  maxb = std::max<int>(maxb, (int)std::min<int64_t>((n + 255) / 256, 64));   // the writer row's blocks
+  hipLaunchKernelGGL(cg_p_img16_kernel, dim3(maxb, a.n + 1), dim3(256), 0, s, a, r, p_old, p_new, n, sc, partials2,
+                     fl, it, img_e);
 }
 
 void launch_fwd_loss16(const FwdLoss16Args& a, int num_cus, hipStream_t s) {

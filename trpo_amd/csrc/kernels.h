@@ -47,6 +47,8 @@ struct Options {
                        // partials are grouped differently, so 1 and 0 are not bit-identical to each other; 2 the
                        // rest of the iteration and the next V image in the same launch, run by the workgroup that
                        // finishes last (cg_step_slabs_kernel, bit-identical to 1; measured slower: DESIGN.md §6)
+  int cg_p_img;        // engine, fused16 path: each CG iteration's p update and the next FVP's V images in one launch
+                       // (fused16.hip cg_p_img16_kernel, bit-identical): 1 (default) on, 0 off
   int rfwd01;          // engine: the FVP's R-forward through layers 0 and 1 in one launch (rfwd.hip) where eligible
                        // (two hidden layers of 256, obs <= 128, the fused tail, X planes): 1 (default) on, 0 off
 };
@@ -265,9 +267,10 @@ void launch_cg_iter(const float* hv, float* x, float* r, float* p, float* z, int
 // single rank, the one-launch FVP: its slab reduction fused with the iteration's z = Hv + damping p and p.z
 // (vec.hip), then the x / r and p updates; P up to kRedBlocks x 64 parameters
 bool cg_fused_reduce_ok(int64_t P);
+// (p_update = false: the caller runs the p update itself, e.g. launch_cg_p_img16)
 void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, float* x, float* r, float* p, float* z,
                           int64_t n, UpdScalars* sc, double* partials, double* partials2, CGFlags* fl, int it,
-                          hipStream_t s);
+                          hipStream_t s, bool p_update = true);
 // cg_fuse_reduce = 2: the whole iteration in one launch (vec.hip cg_step_slabs_kernel): the slab reduction and
 // z / p.z as above, then, in the workgroup that finishes last (an agent-scope ticket that it resets), the x / r and
 // p updates of launch_cg_iter_slabs with bit-identical results, and, when `img` has jobs (the fused16 path), the next
@@ -437,6 +440,9 @@ bool fused16_eligible(int L, const int* w);
 int fused16_obs_chunks(int obs);     // 32-deep k-chunks of V_0's image (obs rounded to 32, 64 or 128)
 int fused16_states_per_group();
 int fused16_groups_per_cu();
+// the CG's p update (cg_p_kernel, bit-identical) into p_new with the V images of p_new (fused16_img_kernel, which = 1)
+void launch_cg_p_img16(const ChainImgArgs& a, const float* r, const float* p_old, float* p_new, int64_t n,
+                       UpdScalars* sc, const double* partials2, CGFlags* fl, int it, int* img_e, hipStream_t s);
 void launch_fused16_img(const ChainImgArgs& a, const float* theta, const float* v, int which, const int* skip,
                         int* img_e, hipStream_t s);
 void launch_fvp_fused16(const Fused16Args& a, int grid, hipStream_t s);

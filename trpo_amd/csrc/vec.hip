@@ -640,15 +640,16 @@ bool cg_fused_reduce_ok(int64_t P) { return (P + kRsCols - 1) / kRsCols <= kRedB
 
 void launch_cg_iter_slabs(const float* slab, int S, int64_t stride, float* hv, float* x, float* r, float* p, float* z,
                           int64_t n, UpdScalars* sc, double* partials, double* partials2, CGFlags* fl, int it,
-                          hipStream_t s) {
+                          hipStream_t s, bool p_update) {
   if (!cg_fused_reduce_ok(n)) throw std::runtime_error("cg_iter_slabs: too many parameters for one partials row");
   const int* skip = &fl->done[it];
   hipLaunchKernelGGL(reduce_slab_kernel<true>, dim3((unsigned)((n + kRsCols - 1) / kRsCols)), dim3(kRsCols * kRsGroups),
                      0, s, slab, S, stride, n, hv, skip, p, z, sc, partials);
   hipLaunchKernelGGL((cg_xr_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, x, r, p, z, n, sc,
                      partials, partials2, it, skip);
-  hipLaunchKernelGGL((cg_p_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, r, p, n, sc,
-                     partials2, fl, it);
+  if (p_update)
+    hipLaunchKernelGGL((cg_p_kernel<float, UpdScalars>), dim3(kRedBlocks), dim3(kRedThreads), 0, s, r, p, n, sc,
+                       partials2, fl, it);
 }
 
 void launch_cg_step_slabs(const CgStepArgs& a, const ChainImgArgs* img, int* img_e, hipStream_t s) {
