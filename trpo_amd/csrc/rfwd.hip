@@ -197,14 +197,15 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
   };
   // Begin chunk c: this wave's DMA into the chunk's slot has landed, then every wave's (the barrier: the chunk is
   // visible, and every wave is past chunk c - 1, whose slot takes chunk c + 3's DMA next).  Completions retire in
-  // issue order; behind chunk c's 8 DMA instructions this wave has issued at least those of chunks c + 1 and c + 2
-  // (16) -- more VMEM operations only where it also issued loads / stores after them -- so vmcnt(16) is a
-  // sufficient wait (first tile's A_0: exactly 16 behind it).  Across a tile boundary more than 63 operations sit
-  // behind (the RZ2 stores): vmcnt(63) there.
-  auto arrive = [&](bool far) __attribute__((always_inline)) {
+  // issue order, so the wait is "at most the number of VMEM operations this wave issued after chunk c's DMA":
+  // chunks c + 1 and c + 2's DMAs (8 + 8) and the 4 RH1 stores of the A chunk among c .. c + 2 = 20 (the first
+  // tile's A_0: only the two DMAs, 16).  Across a tile boundary more than 63 sit behind it (the X loads, the 128
+  // RZ2 stores): vmcnt(63) there.  A smaller count than the true one only waits longer; none is larger.
+  auto arrive = [&](bool far, bool first_a0) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
     if (far) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (first_a0 || (RF_ABL & 8) != 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
     lds_barrier();
   };
   // X's f16 planes, all k-steps, of one state (B operand: lane (state s, half h) holds obs 16 ks + 8 h .. + 7)
@@ -260,7 +261,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         const int cA = 3 * t, sA = (3 * tt) % 4;   // 12 chunks per tq: the slots are static
         const bool far = t == 0 && !first;
         // ---- phase A: RZ1^T slice t ----
-        arrive(far);
+        arrive(far, t == 0 && first);
         dma(cA + 3 < kRfChunks ? cA + 3 : cA + 3 - kRfChunks, (sA + 3) % 4, cA + 3 < kRfChunks ? r0 : r0n);
         const cu32x4* S = slot(sA);
         f32x16 accA = f32x16{};
@@ -336,7 +337,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
           const int cB = cA + 1 + nh, sB = (3 * tt + 1 + nh) % 4;
-          arrive(far);
+          arrive(far, false);
           if (nh == 1 && t == 7) xload(r0n < a.x_mpad ? r0n : 0, xt);   // the next tile's X (none: any valid rows)
           dma(cB + 3 < kRfChunks ? cB + 3 : cB + 3 - kRfChunks, (sB + 3) % 4, cB + 3 < kRfChunks ? r0 : r0n);
           const cu32x4* B = slot(sB);
