@@ -664,8 +664,9 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
     d = O.synthetic_batch(spec, n, seed=13)
     v = np.random.RandomState(14).standard_normal(spec.n_params).astype(np.float32)
     saved = get_option("planes")
-    saved_r0 = get_option("rbwd0")
+    saved_r0, saved_rf = get_option("rbwd0"), get_option("rfwd01")
     set_option("rbwd0", 0)   # the fused layer-1 R-backward needs X's planes: compare the row GEMMs alone
+    set_option("rfwd01", 0)  # so does the one-launch R-forward of layers 0 and 1 (rfwd.hip)
     out = {}
     try:
         for mode in (0, 1):
@@ -680,6 +681,7 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
     finally:
         set_option("planes", saved)
         set_option("rbwd0", saved_r0)
+        set_option("rfwd01", saved_rf)
     for i, what in enumerate(("Hv", "g", "theta")):
         np.testing.assert_array_equal(out[0][i], out[1][i], err_msg=what)
     for k in ("cg_iters", "k", "shs", "lm", "surr_after", "kl_after"):
