@@ -1282,6 +1282,7 @@ struct trpo_engine {
       ra.H1 = H[1];
       ra.c0 = v + offb[0];
       ra.c1 = v + offb[1];
+      ra.V0 = v + offW[0];
       ra.RH1 = RH[1];
       ra.RZ2 = RH[2];
       ra.img = rf_img;

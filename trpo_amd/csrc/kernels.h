@@ -627,6 +627,7 @@ struct Rfwd01Args {
   int x_mpad;
   const int* eX;                     // their scale exponent
   const float *H1, *c0, *c1;         // H1; the tangent biases of layers 0 and 1 (v + offb[l])
+  const float* V0;                   // the direction's layer-0 block, [obs][256] (v + offW[0])
   float *RH1, *RZ2;
   const uint16_t* img;               // rfwd01_img_bytes()
   const unsigned *am_v0, *am_w1, *am_v1;   // the images' running-max slots

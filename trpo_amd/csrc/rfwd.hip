@@ -23,19 +23,27 @@
 // W1 / V1 rows of slice t for output columns 0-127 and 128-255, 32 KB each; the weight chunks from an image built
 // once per FVP in that order by rfwd01_img_kernel, pre-swizzled, so the DMA is a straight copy), each DMA'd three
 // chunks ahead; no other loads in the loop but X once per tile, so the DMA waits are counted exactly (arrive()).
-// Measured (profiles/r6o): 10.46 ms at C4 against 3.93 + 7.99 for the two launches; ablations: without the
+// Measured: 10.46 ms at C4 against 3.93 + 7.99 for the two launches (profiles/r6o); ablations: without the
 // phase-B MFMAs 6.6 ms, without any MFMA 6.0: the 5 KB per state of weights the 128-state tiles re-stream by DMA
-// (50 GB per FVP with H1, ~8 TB/s) bound the launch, and the MFMAs do not hide under it.
+// (50 GB per FVP with H1, ~8 TB/s) and the MFMAs do not overlap (one wave per SIMD).  Then, same box each
+// (profiles/r6s-r6v): the DMA pieces one per k-step among the MFMAs 10.12 -> 9.94; X loaded outside the slice
+// loop, where hipcc no longer drains every DMA in flight before X's first use (its vmcnt(15) ... vmcnt(0) series)
+// 10.22 -> 9.90; the bound-based exponent 9.90 -> 9.25 ms.
 //
 // Scales (f16 hi + lo split, kernels.h f16_scale_exp): X from its plane exponent, V0 / W1 / V1 from their
-// running-max slots; RH1 (made in the launch) per state and slice from the state's max |RH1_t| (an A-operand row
-// is one state, so each state has its own exponent), H1 fixed (|h| <= 1).  Both phase-B segments share a state's
-// product exponent, the smaller of the two segments' (and of every earlier slice's); a state's accumulator row
-// steps down by an exact power of two in the rare case a later slice needs it, and is unscaled at the end.
+// running-max slots; RH1 (made in the launch) per state (an A-operand row is one state, so each state has its own
+// exponent) from a bound fixed at the tile's start, |RH1_sj| <= |RZ1_sj| <= |X_s|_2 max_j |V0_j|_2 + max |c0|
+// (RF_CSB); H1 fixed (|h| <= 1).  Both phase-B segments share a state's product exponent, the smaller of the two,
+// so no slice ever re-scales the accumulators, and the rows are unscaled at the end.  Power-of-two scales change
+// no split and no product: a loose bound costs precision only once a split's low half would fall below f16's
+// normal range, 2^14 below the bound.  (RF_CSB 0: the exponent from each slice's own max, the accumulator rows
+// stepped down by exact powers of two when a later slice needs it: 0.65 ms slower at C4, the re-scaling branch
+// keeping 128 accumulator copies in VGPRs.)
 #include "chain_common.h"
 #include "rowepi.h"
 
 #include <stdexcept>
+#include <type_traits>
 
 namespace trpo {
 namespace {
@@ -45,12 +53,24 @@ typedef __fp16 rf_h2 __attribute__((ext_vector_type(2)));
 #ifndef RF_SGB
 #define RF_SGB 1   // 1: each k-step region issues its next fragments' LDS reads before its MFMAs (sched_group_barrier)
 #endif
-#ifndef RF_PAIR
-#define RF_PAIR 0  // 1: phase B steps in pairs of output tiles, the two accumulator chains interleaved
+#ifndef RF_ILV
+#define RF_ILV 1   // 1: a chunk's 8 DMA instructions issued one per k-step among its MFMAs, not as a burst before them
+#endif
+#ifndef RF_HOIST
+#define RF_HOIST 0  // 1: the slice's H1 and c0 values read from LDS before the phase-A MFMAs, not after them
+#endif
+#ifndef RF_HEAD
+#define RF_HEAD 3   // (RF_CSB 0) a later slice re-scales its state only when it needs an exponent more than RF_HEAD
+                    // below the state's current one (its scaled max then stays < 2^(12 + RF_HEAD) <= 2^15, in f16)
+#endif
+#ifndef RF_CSB
+#define RF_CSB 1    // 1: a state's product exponent from a bound fixed at the tile's start, |RH1| <= |X_s| max_j |V0_j| +
+                    // max |c0| (Cauchy-Schwarz per state): no per-slice exponent, no re-scaling of the accumulators
 #endif
 #ifndef RF_ABL
 #define RF_ABL 0   // timing ablations only (tools/variant.sh), bits: 1 = no phase-B MFMAs, 2 = no phase-B LDS reads,
-                   // 4 = no weight DMA, 8 = no RH1 / RZ2 stores, 16 = no H1 / X loads, 32 = no phase-A MFMAs
+                   // 4 = no weight DMA, 8 = no RH1 / RZ2 stores, 16 = no H1 / X loads, 32 = no phase-A MFMAs,
+                   // 64 = a minimal phase-A epilogue (no tangent, no per-state max: a fixed exponent)
 #endif
 
 constexpr int kRfUnits = 2048;                 // 16-B units of a ring slot / image chunk (32 KB)
@@ -144,6 +164,7 @@ __device__ __forceinline__ void rf_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned v
 
 template <int KS0>   // 16-deep k-steps over obs (obs <= 16 KS0)
 __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Args a) {
+  static_assert(!RF_ILV || KS0 == 8, "interleaved DMA: one instruction per k-step of phase A");
   // the ring: chunk c in slot c % 4.  An A chunk holds V0^T slice t (image units 0..1023) and H1 slice t of the
   // tile's 128 states (units 1024..2047, 256 per wave: row r, column unit cu at r * 8 + (cu ^ ((r >> 1) & 7)), so the
   // epilogue's reads of one column unit over 16 rows hit 16 distinct bank slots); a B chunk the W1 / V1 rows.
@@ -168,39 +189,62 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
     cvec[0][i] = a.c0[i];
     cvec[1][i] = a.c1[i];
   }
+  // RF_CSB: nv0 = max_j |V0[:, j]|_2 and mc0 = max_j |c0_j| (uniform; thread j takes column j)
+  float nv0 = 0.0f, mc0 = 0.0f;
+  if constexpr (RF_CSB) {
+    float q = 0.0f;
+    for (int k = 0; k < a.obs; ++k) {
+      const float x = a.V0[(int64_t)k * 256 + tid];
+      q = fmaf(x, x, q);
+    }
+    float m1 = max32_dpp(sqrtf(q)), m2 = max32_dpp(fabsf(a.c0[tid]));
+    m1 = fmaxf(m1, __shfl_xor(m1, 32));
+    m2 = fmaxf(m2, __shfl_xor(m2, 32));
+    if (lane == 0) {
+      red[0][wv] = m1;
+      red[1][wv] = m2;
+    }
+    __syncthreads();
+    nv0 = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    mc0 = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    __syncthreads();   // red is reused by amax_commit3 at the end
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // ordinary loads retired before the first DMA
   auto slot = [&](int k) -> cu32x4* { return k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3; };
   auto rows_of = [&](int64_t r0w) { return (int)(a.n - r0w < 32 ? (a.n - r0w > 0 ? a.n - r0w : 0) : 32); };
   // chunk c (0..23) into slot sl (= c % 4), 8 DMA instructions per wave: a B chunk from the image; an A chunk half
   // from the image, half this wave's 32 H1 rows of slice t = c / 3 (r0w: the wave's first state of the chunk's tile;
   // rows past n land as zeros)
-  auto dma = [&](int c, int sl, int64_t r0w) __attribute__((always_inline)) {
+  // instruction i (0..7) of that: a B chunk's image piece i; an A chunk's image piece i (i < 4) or H1 piece i - 4
+  // (A: chunk c is an A chunk, c % 3 == 0, known at every call site)
+  auto dma_one = [&](auto A, int c, int sl, int64_t r0w, int i) __attribute__((always_inline)) {
     if constexpr ((RF_ABL & 4) != 0) return;
     const unsigned lds0 = (unsigned)(uintptr_t)slot(sl);
-    const bool A = c % 3 == 0;
-#pragma unroll
-    for (int i = 0; i < (A ? 4 : 8); ++i) {
+    if (!decltype(A)::value || i < 4) {
       const int base = wv * 64 + i * kRfWaves * 64;   // units
       rf_dma16(rimg, (unsigned)(base + lane) * 16u, (unsigned)c * kRfUnits * 16u, lds0 + (unsigned)base * 16u);
-    }
-    if (A) {
-      const int t = c / 3;
+    } else {
+      const int t = c / 3, ih = i - 4;
       const __amdgpu_buffer_rsrc_t rh =
           __builtin_amdgcn_make_buffer_rsrc((void*)(a.H1 + r0w * kRfLd), 0, rows_of(r0w) * kRfLd * 4, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 8 * i + (lane >> 3), cu = (lane & 7) ^ ((r >> 1) & 7);
-        rf_dma16(rh, (unsigned)(r * kRfLd + 4 * cu) * 4u, (unsigned)(32 * t) * 4u,
-                 lds0 + (unsigned)(1024 + wv * 256 + 64 * i) * 16u);
-      }
+      const int r = 8 * ih + (lane >> 3), cu = (lane & 7) ^ ((r >> 1) & 7);
+      rf_dma16(rh, (unsigned)(r * kRfLd + 4 * cu) * 4u, (unsigned)(32 * t) * 4u,
+               lds0 + (unsigned)(1024 + wv * 256 + 64 * ih) * 16u);
     }
   };
+  auto dma = [&](auto A, int c, int sl, int64_t r0w) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_one(A, c, sl, r0w, i);
+  };
+  using kA = std::true_type;
+  using kB = std::false_type;
   // Begin chunk c: this wave's DMA into the chunk's slot has landed, then every wave's (the barrier: the chunk is
   // visible, and every wave is past chunk c - 1, whose slot takes chunk c + 3's DMA next).  Completions retire in
   // issue order, so the wait is "at most the number of VMEM operations this wave issued after chunk c's DMA":
   // chunks c + 1 and c + 2's DMAs (8 + 8) and the 4 RH1 stores of the A chunk among c .. c + 2 = 20 (the first
   // tile's A_0: only the two DMAs, 16).  Across a tile boundary more than 63 sit behind it (the X loads, the 128
-  // RZ2 stores): vmcnt(63) there.  A smaller count than the true one only waits longer; none is larger.
+  // RZ2 stores): vmcnt(63) there, which also covers the next tile's X loads (128 stores were issued after them).
+  // A smaller count than the true one only waits longer; none is larger.
   auto arrive = [&](bool far, bool first_a0) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
     if (far) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
@@ -232,11 +276,14 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 
   f16x8 xt[KS0][2];   // X of this wave's 32 states, the whole tile
   xload((int64_t)blockIdx.x * kRfTile + wv * 32, xt);   // (grid <= tiles: a real tile)
+  // the first tile's X waited for here, where hipcc's own s_waitcnt bookkeeping sees it: the later tiles' X loads
+  // are followed by the 128 RZ2 stores (more than vmcnt's 63), so hipcc puts no wait in front of X's uses
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
   {
     const int64_t r0f = (int64_t)blockIdx.x * kRfTile + wv * 32;
-    dma(0, 0, r0f);
-    dma(1, 1, r0f);
-    dma(2, 2, r0f);
+    dma(kA{}, 0, 0, r0f);
+    dma(kB{}, 1, 1, r0f);
+    dma(kB{}, 2, 2, r0f);
   }
 
   float mR = 0.0f, mZ = 0.0f;   // running max |RH1|, |RZ2| of this lane
@@ -251,6 +298,22 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = f32x16{};
     int Ps = 0;   // this lane's state's product exponent (set by slice 0, lowered when a later slice needs it)
+    if constexpr (RF_CSB) {
+      // |RH1_sj| <= |RZ1_sj| <= |X_s|_2 |V0_j|_2 + |c0_j|; |X_s| from the hi plane (|x| <= |hi| (1 + 2^-10)),
+      // 1 % over for that and for the split products' rounding
+      float q = 0.0f;
+#pragma unroll
+      for (int ks = 0; ks < KS0; ++ks) {
+        const f16x8 x8 = xt[ks][0];
+        q = __builtin_amdgcn_fdot2(__builtin_shufflevector(x8, x8, 0, 1), __builtin_shufflevector(x8, x8, 0, 1), q, false);
+        q = __builtin_amdgcn_fdot2(__builtin_shufflevector(x8, x8, 2, 3), __builtin_shufflevector(x8, x8, 2, 3), q, false);
+        q = __builtin_amdgcn_fdot2(__builtin_shufflevector(x8, x8, 4, 5), __builtin_shufflevector(x8, x8, 4, 5), q, false);
+        q = __builtin_amdgcn_fdot2(__builtin_shufflevector(x8, x8, 6, 7), __builtin_shufflevector(x8, x8, 6, 7), q, false);
+      }
+      q = xadd_f<true>(q);   // the state's other 8 obs of each 16 (lane s + 32)
+      const float bnd = __builtin_ldexpf(sqrtf(q), -eX) * nv0 * 1.01f + mc0;
+      Ps = min(bnd > 0.0f ? f16_scale_exp(bnd) + eW : 1000, f16_scale_exp(1.0f) + eV);
+    }
     // accumulator register r of this lane holds state 8 (r >> 2) + 4 h + (r & 3): its exponent comes through LDS
     int* px = pex[wv];
 #pragma unroll 1
@@ -262,8 +325,23 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         const bool far = t == 0 && !first;
         // ---- phase A: RZ1^T slice t ----
         arrive(far, t == 0 && first);
-        dma(cA + 3 < kRfChunks ? cA + 3 : cA + 3 - kRfChunks, (sA + 3) % 4, cA + 3 < kRfChunks ? r0 : r0n);
+        const int cA3 = cA + 3 < kRfChunks ? cA + 3 : cA + 3 - kRfChunks;
+        const int64_t rA3 = cA + 3 < kRfChunks ? r0 : r0n;
+        if (!RF_ILV) dma(kA{}, cA3, (sA + 3) % 4, rA3);
         const cu32x4* S = slot(sA);
+        float hv[16], cb[16];
+        auto ldh = [&]() __attribute__((always_inline)) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cu = 2 * j + h;
+            const f32x4 v4 = __builtin_bit_cast(f32x4, S[1024 + wv * 256 + s * 8 + (cu ^ ((s >> 1) & 7))]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hv[4 * j + i] = v4[i];
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cb[r] = cvec[0][32 * t + 8 * (r >> 2) + 4 * h + (r & 3)];
+        };
+        if (RF_HOIST) ldh();
         f32x16 accA = f32x16{};
         // fragments one k-step ahead of the MFMAs (sched barriers keep the compiler from hoisting them all)
         f16x8 fa[2][2];
@@ -276,6 +354,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 #pragma unroll
         for (int ks = 0; ks < KS0; ++ks) {
           __builtin_amdgcn_sched_barrier(0);
+          if (RF_ILV) dma_one(kA{}, cA3, (sA + 3) % 4, rA3, ks);
           if (ks + 1 < KS0) lda(ks + 1, fa[(ks + 1) & 1]);
           if constexpr ((RF_ABL & 32) == 0) accA = rf_mfma3(fa[ks & 1][0], fa[ks & 1][1], xt[ks][0], xt[ks][1], accA);
           if (RF_SGB && ks + 1 < KS0) {
@@ -285,20 +364,17 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- epilogue: RH1 slice t (stored), the state's max -> its phase-B product exponent ----
-        float hv[16], rh[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cu = 2 * j + h;
-          const f32x4 v4 = __builtin_bit_cast(f32x4, S[1024 + wv * 256 + s * 8 + (cu ^ ((s >> 1) & 7))]);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) hv[4 * j + i] = v4[i];
-        }
+        if (!RF_HOIST) ldh();
+        float rh[16];
         float mt = 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float cb = cvec[0][32 * t + 8 * (r >> 2) + 4 * h + (r & 3)];
-          rh[r] = one_minus_sq(hv[r]) * (accA[r] * uA + cb);
-          mt = fmaxf(mt, fabsf(rh[r]));
+          if constexpr ((RF_ABL & 64) != 0) {
+            rh[r] = accA[r] * uA;
+          } else {
+            rh[r] = one_minus_sq(hv[r]) * (accA[r] * uA + cb[r]);
+            mt = fmaxf(mt, fabsf(rh[r]));
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4 && (RF_ABL & 8) == 0; ++j)
@@ -306,14 +382,18 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
               __builtin_bit_cast(cu32x4, f32x4{rh[4 * j], rh[4 * j + 1], rh[4 * j + 2], rh[4 * j + 3]}), rrh, hlane,
               (32 * t + 8 * j) * 4, 0);
         mR = fmaxf(mR, mt);
-        mt = xmax_f<true>(mt);   // the state's max over the slice (lanes s and s + 32)
-        const int Pt = min(mt > 0.0f ? f16_scale_exp(mt) + eW : 1000, f16_scale_exp(1.0f) + eV);
-        if (t == 0) {
+        if constexpr ((RF_ABL & 64) == 0 && !RF_CSB) mt = xmax_f<true>(mt);   // the state's max over the slice
+        const int Pt = (RF_ABL & 64) ? 2 : min(mt > 0.0f ? f16_scale_exp(mt) + eW : 1000, f16_scale_exp(1.0f) + eV);
+        if constexpr (RF_CSB) {
+          // Ps fixed for the tile
+        } else if (t == 0) {
           Ps = Pt;
-        } else if (__builtin_amdgcn_ballot_w64(Pt < Ps) != 0) {
-          // rare: a state whose slice is larger than all its earlier ones; its accumulator rows step down by an
-          // exact power of two (the other states' by 2^0)
-          if (h == 0) px[s] = Pt < Ps ? Pt - Ps : 0;
+        } else if (__builtin_amdgcn_ballot_w64(Pt < Ps - RF_HEAD) != 0) {
+          // rare: a state whose slice is more than 2^RF_HEAD larger than its exponent allows; its accumulator rows
+          // step down by an exact power of two (the other states' by 2^0).  Power-of-two scales change no split and
+          // no product, so the headroom only bounds f16's range (the per-slice rule, RF_HEAD = 0, re-scaled in most
+          // slices of random data: 1.1 ms of the launch's 10)
+          if (h == 0) px[s] = Pt < Ps - RF_HEAD ? Pt - Ps : 0;
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
           float f[16];
@@ -323,7 +403,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
           for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][r] *= f[r];
-          Ps = min(Ps, Pt);
+          Ps = Pt < Ps - RF_HEAD ? Pt : Ps;
           __builtin_amdgcn_wave_barrier();
         }
         const float sR = __builtin_ldexpf(1.0f, Ps - eW), sH = __builtin_ldexpf(1.0f, Ps - eV);
@@ -338,8 +418,9 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         for (int nh = 0; nh < 2; ++nh) {
           const int cB = cA + 1 + nh, sB = (3 * tt + 1 + nh) % 4;
           arrive(far, false);
-          if (nh == 1 && t == 7) xload(r0n < a.x_mpad ? r0n : 0, xt);   // the next tile's X (none: any valid rows)
-          dma(cB + 3 < kRfChunks ? cB + 3 : cB + 3 - kRfChunks, (sB + 3) % 4, cB + 3 < kRfChunks ? r0 : r0n);
+          const int cB3 = cB + 3 < kRfChunks ? cB + 3 : cB + 3 - kRfChunks;
+          const int64_t rB3 = cB + 3 < kRfChunks ? r0 : r0n;
+          if (!RF_ILV) dma(kB{}, cB3, (sB + 3) % 4, rB3);
           const cu32x4* B = slot(sB);
           // step k = 4 uu + tn; its W / V fragments loaded one step ahead
           f16x8 fb[2][4];
@@ -355,6 +436,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             __builtin_amdgcn_sched_barrier(0);
+            if (RF_ILV) dma_one(kB{}, cB3, (sB + 3) % 4, rB3, k);
             if (k + 1 < 8 && (RF_ABL & 2) == 0) ldb(k + 1, fb[(k + 1) & 1]);
             const int uu = k >> 2, tn = k & 3;
             const f16x8(&f)[4] = fb[k & 1];
@@ -373,6 +455,7 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
         }
       }
     }
+    xload(r0n < a.x_mpad ? r0n : 0, xt);   // the next tile's X (none: any valid rows), ahead of the RZ2 stores
     // ---- RZ2 = acc 2^-P + c1: lane (column 32 tn + s, states 8 j + 4 h + i) ----
     if (h == 0) px[s] = Ps;
     __builtin_amdgcn_wave_barrier();
