@@ -109,6 +109,8 @@ def tag_flops(tag: str, widths, n: int) -> float:
         return 2.0 * n * sum(widths[l] * widths[l + 1] for l in range(len(widths) - 1))
     if tag == "fvp_rfwd01":           # rfwd.hip: X V0 (2 a0 a1) + RH1 W1 + H1 V1 (4 a1 a2)
         return 2.0 * n * widths[0] * widths[1] + 4.0 * n * widths[1] * widths[2]
+    if tag in ("fwd_l01", "ls_fwd_l01"):   # rfwd.hip fwd01_kernel: X W0 + H1 W1
+        return 2.0 * n * (widths[0] * widths[1] + widths[1] * widths[2])
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
         return 0.0
@@ -133,7 +135,7 @@ def tag_flops(tag: str, widths, n: int) -> float:
 def tag_is_split(tag: str, widths) -> bool:
     """Whether the kernel behind a tag runs on the split-bf16 MFMA path (gemm.hip dispatch rules)."""
     from trpo_amd._lib import get_option
-    if tag in ("fvp_chain", "fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01"):
+    if tag in ("fvp_chain", "fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01", "fwd_l01", "ls_fwd_l01"):
         return True
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():
@@ -164,7 +166,8 @@ def tag_products(tag: str, widths) -> int:
     split (6), fused16.hip the scaled f16 hi+lo (3), the row GEMMs the engine's split option."""
     if tag == "fvp_chain" or (tag == "fvp_fused" and not fused16_used(widths)):
         return 6
-    return 3 if tag in ("fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01") else split_products()
+    return 3 if tag in ("fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01", "fwd_l01", "ls_fwd_l01") \
+        else split_products()
 
 
 def tag_peak(tag: str, widths) -> float:
@@ -184,6 +187,10 @@ def tag_bytes(tag: str, widths, n: int) -> float:
         return 4.0 * n * sum(widths)
     if tag == "fvp_rfwd01":           # X (its f16 planes) ; H1 ; RH1, RZ2 out
         return 4.0 * n * (widths[0] + 2 * widths[1] + widths[2])
+    if tag == "fwd_l01":              # X (its f16 planes) ; H1, H2 out
+        return 4.0 * n * (widths[0] + widths[1] + widths[2])
+    if tag == "ls_fwd_l01":           # X ; H2 out (H1 stays on chip)
+        return 4.0 * n * (widths[0] + widths[2])
     if tag == "ls_fwd":               # X ; pi_old (the row terms are O(n))
         return 4.0 * n * (widths[0] + widths[-1])
     if tag == "fwd":                  # X ; pi_old ; H_l, P, D_L, DS_L out
@@ -240,7 +247,7 @@ def tail_used(widths) -> bool:
 def tag_x_bytes(tag: str, widths, n: int) -> float:
     """SURVEY.md §8(d)'s algorithmic bytes of one launch: the states' X rows (N*obs*4) when the kernel
     reads X, else 0 (every other operand is an intermediate the algorithm need not materialise)."""
-    if tag in ("fvp_chain", "fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01"):
+    if tag in ("fvp_chain", "fvp_fused", "pg_fused", "fwd", "ls_fwd", "fvp_rfwd01", "fwd_l01", "ls_fwd_l01"):
         return 4.0 * n * widths[0]
     role, _, l = tag.rpartition("_l")
     if not l.isdigit():

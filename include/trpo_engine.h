@@ -229,6 +229,8 @@ int trpo_discount(const double* x, const uint8_t* episode_starts, int64_t n, dou
  * bit-identical: 1 = on, the default; 0 = two launches).
  * "rfwd01" (the FVP's R-forward through layers 0 and 1 as one launch, rfwd.hip, where two hidden layers of 256
  * with obs <= 128 run the fused tail: 1 = on, the default; 0 = the plane and row GEMM launches).
+ * "fwd01" (the prepare and line-search forwards through layers 0 and 1 as one launch, rfwd.hip, at the same
+ * shapes: 1 = on, the default; 0 = the plane and row GEMM launches).
  * "ls_fused" = 2 mixes two forwards inside one line search (loss_before from the per-layer forward, the
  * trials' losses from fwd_loss16); it exists for A/B timing and is held to the same parity tests.
  * Rejected variants (other tiles, last-layer fusions, 16-bit E planes, a second stream) were removed

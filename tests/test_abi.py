@@ -94,3 +94,4 @@ def test_every_documented_option_is_known():
     assert get_option("graphs") == 1
     assert get_option("hbwd2") == 2 and get_option("head_fwd") == 1 and get_option("ls_fused") == 1
     assert get_option("cg_fuse_reduce") == 1 and get_option("rfwd01") == 1 and get_option("cg_p_img") == 1
+    assert get_option("fwd01") == 1

@@ -293,6 +293,7 @@ def test_bad_actions_fail_loudly(gpu_available):
     {"cg_fuse_reduce": 2},                                    # the whole CG iteration after the FVP in one launch
     {"cg_p_img": 0},                                          # the CG's p update and the V images as two launches
     {"rfwd01": 0},                                            # R-forward of layers 0 / 1 as two launches (C4 dims)
+    {"fwd01": 0},                                             # the forward's layers 0 / 1 as two launches (C4 dims)
 ], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_kernel_variants_parity(gpu_available, opts):
     """Every selectable kernel variant reproduces the golden FVP / gradient / update at C3 and
@@ -302,7 +303,7 @@ def test_kernel_variants_parity(gpu_available, opts):
     defaults = {k: get_option(k) for k in ("split_mfma", "split_wg", "chain", "split_f16", "split_min_k", "fused",
                                            "low_seg", "planes", "tail", "rbwd0", "hbwd2", "head_fwd",
                                            "splits", "pg_splits", "ls_fused", "cg_fuse_reduce", "rfwd01",
-                                           "cg_p_img")}
+                                           "cg_p_img", "fwd01")}
     try:
         for k, v in opts.items():
             set_option(k, v)
@@ -664,9 +665,10 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
     d = O.synthetic_batch(spec, n, seed=13)
     v = np.random.RandomState(14).standard_normal(spec.n_params).astype(np.float32)
     saved = get_option("planes")
-    saved_r0, saved_rf = get_option("rbwd0"), get_option("rfwd01")
+    saved_r0, saved_rf, saved_f = get_option("rbwd0"), get_option("rfwd01"), get_option("fwd01")
     set_option("rbwd0", 0)   # the fused layer-1 R-backward needs X's planes: compare the row GEMMs alone
-    set_option("rfwd01", 0)  # so does the one-launch R-forward of layers 0 and 1 (rfwd.hip)
+    set_option("rfwd01", 0)  # so do the one-launch R-forward and forward of layers 0 and 1 (rfwd.hip)
+    set_option("fwd01", 0)
     out = {}
     try:
         for mode in (0, 1):
@@ -682,6 +684,7 @@ def test_planes_bit_identical_to_register_split(gpu_available, obs, hidden, A, n
         set_option("planes", saved)
         set_option("rbwd0", saved_r0)
         set_option("rfwd01", saved_rf)
+        set_option("fwd01", saved_f)
     for i, what in enumerate(("Hv", "g", "theta")):
         np.testing.assert_array_equal(out[0][i], out[1][i], err_msg=what)
     for k in ("cg_iters", "k", "shs", "lm", "surr_after", "kl_after"):
@@ -1114,3 +1117,68 @@ def test_rfwd01_vs_two_launches_and_oracle(gpu_available, n, case):
         assert rel_l2(hv[1][sl], ref[sl]) <= bar, (case, rel_l2(hv[1][sl], ref[sl]), rel_l2(hv[0][sl], ref[sl]), bar)
     if case != "illcond":
         assert_vec_close(hv[1], hv[0], REL, f"rfwd01 {case} vs two launches")
+
+
+@pytest.mark.parametrize("n,case", [
+    (1, "plain"), (129, "plain"), (3001, "plain"), (40_000, "plain"),
+    (3001, "tanh_sat"), (3001, "mixed"), (3001, "illcond"),   # as in test_rfwd01_vs_two_launches_and_oracle
+])
+def test_fwd01_vs_per_layer_and_oracle(gpu_available, n, case):
+    """The prepare / line-search forward of layers 0 / 1 in one launch (rfwd.hip fwd01_kernel) at C4 widths: the
+    policy gradient and Hv (both read the prepare pass's H1 / H2) against the float64 oracle, per block at
+    max(1e-5, 4 x the float32 graph's error), and with one update (its line search reads the trial forward)
+    against the per-layer forwards (fwd01 = 0): g, Hv, the step and the losses at 1e-5, k and the CG count exact."""
+    from trpo_amd import Engine, UpdateParams
+    from trpo_amd._lib import get_option, set_option
+    spec = O.PolicySpec(128, [256, 256], 18)
+    dd = O.synthetic_batch(spec, n, seed=51)
+    th = dd["theta"].astype(np.float32).copy()
+    X = dd["X"].astype(np.float32).copy()
+    v = np.random.RandomState(52).standard_normal(spec.n_params).astype(np.float32)
+    (w0, b0), _, _ = _block_slices(spec)
+    if case == "tanh_sat":
+        th[w0] *= 20.0
+    elif case == "mixed":   # rfwd01's case: W_0's last rows zero, so X W_0 stays exact for the large states
+        th64 = th.astype(np.float64)
+        W0 = th64[w0].reshape(spec.obs_dim, spec.hidden[0])
+        W0[-3:, :] = 0.0
+        th[w0] = W0.reshape(-1).astype(np.float32)
+        rs = np.random.RandomState(53)
+        for i in range(5, n, 29):
+            X[i, -3:] = (2.0 ** 15 * rs.standard_normal(3)).astype(np.float32)
+    elif case == "illcond":
+        X[::97] *= 4096.0
+    adv = dd["advant"].astype(np.float32)
+    dflt = get_option("fwd01")
+    out = {}
+    try:
+        for mode in (1, 0):
+            set_option("fwd01", mode)
+            e = Engine(spec.obs_dim, spec.hidden, spec.n_actions, max_rows=n)
+            e.set_flat(th)
+            e.set_batch(X, dd["actions"], adv, dd["old_dist"])
+            g, hv = e.policy_grad(), e.fvp(v, 0.0)
+            st = e.update(UpdateParams(cg_iters=10, residual_tol=0.0))
+            out[mode] = (g, hv, e.get_flat(), st)
+            e.close()
+    finally:
+        set_option("fwd01", dflt)
+    th64, X64 = th.astype(np.float64), X.astype(np.float64)
+    gref = O.policy_grad(th64, X64, dd["actions"], dd["advant"], dd["old_dist"], spec)
+    g32 = O.policy_grad(th, X, dd["actions"], dd["advant"], dd["old_dist"], spec, dtype=np.float32)
+    href = O.fvp_undamped(th64, X64, v.astype(np.float64), spec)
+    h32 = O.fvp_undamped(th, X, v, spec, dtype=np.float32)
+    for sl in [s_ for blk in _block_slices(spec) for s_ in blk]:
+        gb = max(REL, 4.0 * rel_l2(g32[sl], gref[sl]))
+        hb = max(REL, 4.0 * rel_l2(h32[sl], href[sl]))
+        assert rel_l2(out[1][0][sl], gref[sl]) <= gb, (case, "g", rel_l2(out[1][0][sl], gref[sl]), gb)
+        assert rel_l2(out[1][1][sl], href[sl]) <= hb, (case, "Hv", rel_l2(out[1][1][sl], href[sl]), hb)
+    if case != "illcond":
+        assert_vec_close(out[1][0], out[0][0], REL, f"fwd01 {case} g vs per-layer")
+        assert_vec_close(out[1][1], out[0][1], REL, f"fwd01 {case} Hv vs per-layer")
+        assert_vec_close(out[1][2], out[0][2], REL, f"fwd01 {case} theta vs per-layer")
+        for k in ("k", "cg_iters"):
+            assert out[1][3][k] == out[0][3][k], (case, k)
+        for k in ("surr_after", "kl_after"):   # (kl of the accepted step: max_kl 0.01 is its scale)
+            a1, a0 = float(out[1][3][k]), float(out[0][3][k])
+            assert abs(a1 - a0) <= REL * max(abs(a0), 1e-2), (case, k, a1, a0)

@@ -202,10 +202,16 @@ struct trpo_engine {
   // layer 1's R-backward (and the policy gradient's backward into layer 0) fused with layer 0's weight
   // gradient (rbwd0.hip): f16 split with X's planes, obs <= 128, first hidden width <= 256
   uint16_t* rf_img = nullptr;   // rfwd.hip's chunk image (V0^T, W1, V1 in the kernel's LDS order), per FVP
+  uint16_t* fw_img = nullptr;   // rfwd.hip's forward image (W0^T, W1), per forward
   // the R-forward through layers 0 and 1 in one launch: X's planes, the fused tail (RZ2 is its pre-activation)
   bool use_rfwd01() const {
     return g_options.rfwd01 != 0 && rf_img && f16 && split_on() && use_tail() && planes_l0() &&
            rfwd01_eligible(L, w.data(), wp.data()) && (int64_t)x_mpad <= ((int64_t)1 << 23);
+  }
+  // the forward's layers 0 and 1 in one launch (rfwd.hip fwd01_kernel): tanh layers of 256, X on its planes
+  bool use_fwd01() const {
+    return g_options.fwd01 != 0 && fw_img && f16 && split_on() && planes_l0() && fwd01_eligible(L, w.data(), wp.data()) &&
+           (int64_t)x_mpad <= ((int64_t)1 << 23);
   }
   bool use_rbwd0() const {
     return g_options.rbwd0 != 0 && f16 && x_planes && rbwd0_geom() && g_options.planes != 0 && split_on() &&
@@ -441,6 +447,7 @@ struct trpo_engine {
     amax = dalloc<unsigned>((size_t)(1 + 8 * kMaxLayers) * kAmaxSlot);
     if (L >= 2 && tail_eligible(wp[L - 1], wp[L])) tail_planes = dalloc<uint16_t>((size_t)2 * 2 * 32 * kTailK);
     if (rfwd01_eligible(L, w.data(), wp.data())) rf_img = dalloc<uint16_t>(rfwd01_img_bytes() / 2);
+    if (fwd01_eligible(L, w.data(), wp.data())) fw_img = dalloc<uint16_t>(fwd01_img_bytes() / 2);
     // allocated last: the big activation buffers keep the placement the kernels were tuned on
     stage = dalloc<float>((size_t)cap * std::max(std::max(wp[0], wp[L]), 2));
     if (f16 && (planes_geom_l0() || rbwd0_geom())) {
@@ -916,7 +923,37 @@ struct trpo_engine {
   // epilogue is `head`; hidden activations go to `hout`
   void forward(const std::vector<float*>& wf, const std::vector<uint16_t*>& wf3, const float* th,
                const std::vector<float*>& hout, RowEpi head, const char* tag) {
-    for (int l = 0; l < L; ++l) {
+    int l_first = 0;
+    if (use_fwd01()) {   // layers 0 and 1 in one launch; H1 stored by the prepare pass only (the FVP reads it)
+      const bool wt = &wf == &WFt;
+      char t[32];
+      std::snprintf(t, sizeof t, "%s_img", tag);
+      {
+        Scope sp(this, t);
+        launch_fwd01_img(th, offW[0], offW[1], w[0], wt ? am_wt(0) : am_w(0), wt ? am_wt(1) : am_w(1), fw_img, stream);
+        check_launch();
+      }
+      Fwd01Args fa{};
+      fa.n = n;
+      fa.obs = w[0];
+      fa.Xh = Xh;
+      fa.Xl = Xl;
+      fa.x_mpad = x_mpad;
+      fa.eX = pl_e;
+      fa.b0 = th + offb[0];
+      fa.b1 = th + offb[1];
+      fa.H1 = head == RowEpi::kPrepHead ? hout[1] : nullptr;
+      fa.H2 = hout[2];
+      fa.img = fw_img;
+      fa.am_w0 = wt ? am_wt(0) : am_w(0);
+      fa.am_w1 = wt ? am_wt(1) : am_w(1);
+      std::snprintf(t, sizeof t, "%s_l01", tag);
+      Scope sp(this, t);
+      launch_fwd01(fa, num_cus, stream);
+      check_launch();
+      l_first = 2;
+    }
+    for (int l = l_first; l < L; ++l) {
       RowGemmArgs a = row_args(w[l + 1], wp[l + 1]);
       a.nseg = 1;
       a.seg[0] = GemmSeg{l == 0 ? X : hout[l], wf[l], wp[l], wp[l + 1], wp[l]};
@@ -2779,6 +2816,7 @@ static int* option_slot(const std::string& k) {
   if (k == "ls_fused") return &g_options.ls_fused;
   if (k == "cg_fuse_reduce") return &g_options.cg_fuse_reduce;
   if (k == "rfwd01") return &g_options.rfwd01;
+  if (k == "fwd01") return &g_options.fwd01;
   if (k == "cg_p_img") return &g_options.cg_p_img;
   throw ArgError("unknown option " + k);
 }

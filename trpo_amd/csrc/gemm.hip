@@ -41,7 +41,7 @@ Options g_options = {env_int("TRPO_SPLIT_MFMA", 5), env_int("TRPO_SPLIT_WG", 1),
                      env_int("TRPO_HEAD_FWD", 1), env_int("TRPO_SPLITS", 0),
                      env_int("TRPO_PG_SPLITS", 0), env_int("TRPO_LS_FUSED", 1),
                      env_int("TRPO_CG_FUSE_REDUCE", 1), env_int("TRPO_CG_P_IMG", 1),
-                     env_int("TRPO_RFWD01", 1)};
+                     env_int("TRPO_RFWD01", 1), env_int("TRPO_FWD01", 1)};
 
 namespace {
 

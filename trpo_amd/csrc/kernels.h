@@ -50,6 +50,7 @@ struct Options {
   int cg_p_img;        // engine, fused16 path: each CG iteration's p update and the next FVP's V images in one launch
                        // (fused16.hip cg_p_img16_kernel, bit-identical): 1 (default) on, 0 off
   int rfwd01;          // engine: the FVP's R-forward through layers 0 and 1 in one launch (rfwd.hip) where eligible
+  int fwd01;           // engine: the prepare / line-search forward through layers 0 and 1 in one launch (rfwd.hip)
                        // (two hidden layers of 256, obs <= 128, the fused tail, X planes): 1 (default) on, 0 off
 };
 
@@ -634,6 +635,25 @@ struct Rfwd01Args {
   unsigned *am_rh1, *am_rz2;         // running max |RH1|, |RZ2| (atomicMax'd)
   const int* skip;
 };
+// The policy forward through layers 0 and 1 in one launch (rfwd.hip, option fwd01): H1 = tanh(X W0 + b0) (stored
+// when H1 is set: the prepare pass) and H2 = tanh(H1 W1 + b1), same shapes as rfwd01, W0 / W1 from a per-forward
+// chunk image (launch_fwd01_img).
+struct Fwd01Args {
+  int64_t n;
+  int obs;
+  const uint16_t *Xh, *Xl;           // X's k-blocked f16 planes, x_mpad rows per 32-k block
+  int x_mpad;
+  const int* eX;
+  const float *b0, *b1;              // th + offb[0], th + offb[1]
+  float *H1, *H2;                    // H1: NULL = not stored (the line search)
+  const uint16_t* img;               // fwd01_img_bytes()
+  const unsigned *am_w0, *am_w1;     // the weights' running-max slots (the image's scales)
+};
+bool fwd01_eligible(int L, const int* w, const int* wp);
+size_t fwd01_img_bytes();
+void launch_fwd01_img(const float* th, int64_t offW0, int64_t offW1, int obs, const unsigned* am_w0,
+                      const unsigned* am_w1, uint16_t* img, hipStream_t s);
+void launch_fwd01(const Fwd01Args& a, int num_cus, hipStream_t s);
 bool rfwd01_eligible(int L, const int* w, const int* wp);
 size_t rfwd01_img_bytes();
 void launch_rfwd01_img(const float* theta, const float* v, int64_t offV0, int64_t offW1, int obs,

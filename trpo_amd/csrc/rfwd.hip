@@ -484,6 +484,218 @@ __global__ void __launch_bounds__(kRfWaves * 64, 1) rfwd01_kernel(const Rfwd01Ar
   amax_commit3<true>(a.am_rh1, mR, a.am_rz2, mZ, nullptr, 0.0f, red);
 }
 
+
+// ---- the policy forward through layers 0 and 1 in one launch (option fwd01): trpo_inksci.py:38-40 ----------------
+//   H1 = tanh(X W0 + b0) (stored by the prepare pass only) ;  H2 = tanh(H1 W1 + b1) (stored)
+// rfwd01's structure with one phase-B segment and no H1 input: per slice t an A chunk (W0^T slice t, 16 KB, the
+// layout of rfwd01's V0^T chunk) and a B chunk (W1 rows of slice t, all 256 columns, 32 KB: [plane][column r
+// 0..255][unit u ^ ((r >> 2) & 3)], u = 2 uu + h holding W1[32 t + 16 uu + 4 h + 8 (q >> 2) + (q & 3)][r]), 16
+// chunks per tile through the same 4-slot ring.  |h| <= 1, so H1's scale is fixed (2^11) and no exponent is
+// tracked per state.
+constexpr int kFwChunks = 16;
+
+__global__ void __launch_bounds__(256) fwd01_img_kernel(const float* __restrict__ th, int64_t offW0, int64_t offW1,
+                                                        int obs, const unsigned* am_w0, const unsigned* am_w1,
+                                                        uint16_t* __restrict__ img) {
+  const int eW0 = amax_exp(am_w0), eW1 = amax_exp(am_w1);
+  const int gid = blockIdx.x * 256 + threadIdx.x;   // 8 slices x (512 A units + 1024 B units)
+  const int t = gid / 1536, rem = gid % 1536;
+  if (t >= 8) return;
+  float x[8];
+  cu32x4* dst;
+  int plane_units;
+  float sc;
+  if (rem < 512) {   // A_t: feature f, unit u
+    const int f = rem >> 4, u = rem & 15, ks = u >> 1, h = u & 1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 16 * ks + 8 * h + q;
+      x[q] = k < obs ? th[offW0 + (int64_t)k * 256 + 32 * t + f] : 0.0f;
+    }
+    sc = __builtin_ldexpf(1.0f, eW0);
+    dst = reinterpret_cast<cu32x4*>(img) + (size_t)(2 * t) * kRfUnits + f * 16 + (u ^ (f & 15));
+    plane_units = 512;
+  } else {   // B_t: column r, unit u
+    const int b = rem - 512, r = b >> 2, u = b & 3, uu = u >> 1, h = u & 1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 32 * t + 16 * uu + 4 * h + 8 * (q >> 2) + (q & 3);
+      x[q] = th[offW1 + (int64_t)k * 256 + r];
+    }
+    sc = __builtin_ldexpf(1.0f, eW1);
+    dst = reinterpret_cast<cu32x4*>(img) + (size_t)(2 * t + 1) * kRfUnits + r * 4 + (u ^ ((r >> 2) & 3));
+    plane_units = 1024;
+  }
+  f16x8 hi, lo;
+  rf_split8(x, sc, hi, lo);
+  dst[0] = __builtin_bit_cast(cu32x4, hi);
+  dst[plane_units] = __builtin_bit_cast(cu32x4, lo);
+}
+
+template <int KS0, bool PREP>
+__global__ void __launch_bounds__(kRfWaves * 64, 1) fwd01_kernel(const Fwd01Args a) {
+  __shared__ cu32x4 q0[kRfUnits], q1[kRfUnits], q2[kRfUnits], q3[kRfUnits];
+  __shared__ float cvec[2][256];      // the biases b0, b1
+  const int tid = threadIdx.x, lane = tid & 63, s = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int eX = __builtin_amdgcn_readfirstlane(*a.eX);
+  const int eW0 = __builtin_amdgcn_readfirstlane(amax_exp(a.am_w0));
+  const int eW1 = __builtin_amdgcn_readfirstlane(amax_exp(a.am_w1));
+  const float uA = __builtin_ldexpf(1.0f, -(eX + eW0));
+  const int P = f16_scale_exp(1.0f) + eW1;   // products of H1 (scaled 2^(P - eW1) = 2^11) and W1 (2^eW1)
+  const float sH = __builtin_ldexpf(1.0f, P - eW1), uP = __builtin_ldexpf(1.0f, -P);
+  const int64_t ntiles = (a.n + kRfTile - 1) / kRfTile;
+  const __amdgpu_buffer_rsrc_t rimg =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, kFwChunks * kRfUnits * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxh = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xh, 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxl = __builtin_amdgcn_make_buffer_rsrc((void*)a.Xl, 0, 0x7ffffff0, 0x00020000);
+  for (int i = tid; i < 256; i += kRfWaves * 64) {
+    cvec[0][i] = a.b0[i];
+    cvec[1][i] = a.b1[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // ordinary loads retired before the first DMA
+  auto slot = [&](int k) -> cu32x4* { return k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3; };
+  auto rows_of = [&](int64_t r0w) { return (int)(a.n - r0w < 32 ? (a.n - r0w > 0 ? a.n - r0w : 0) : 32); };
+  // piece i of chunk c's DMA into slot sl: an A chunk has 4 pieces per wave (16 KB), a B chunk 8 (32 KB)
+  auto dma_one = [&](int c, int sl, int i) __attribute__((always_inline)) {
+    const unsigned lds0 = (unsigned)(uintptr_t)slot(sl);
+    const int base = wv * 64 + i * kRfWaves * 64;   // units
+    rf_dma16(rimg, (unsigned)(base + lane) * 16u, (unsigned)c * kRfUnits * 16u, lds0 + (unsigned)base * 16u);
+  };
+  // Begin chunk c (see rfwd01_kernel's arrive()).  Operations behind chunk c's DMA, S = 4 H1 stores per A chunk
+  // (prepare) or 0: an A chunk 8 + S (chunk c - 2: the next B chunk's DMA and its stores) + 4 (chunk c - 1: an A
+  // chunk's DMA) = 12 + S; a B chunk S + 4 + 8 + S = 12 + 2 S.  The first tile's chunk 0: 12, chunk 1: 12 + S.
+  // Across a tile boundary (chunks 0, 1, 2 of a later tile) the X loads and the 128 H2 stores: vmcnt(63).
+  // (A count below the true one only waits longer: 12 + S and 12 + 2 S are 16 / 20 or 12 / 12.)
+  constexpr int S = PREP ? 4 : 0;
+  auto arrive = [&](int cnt) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (cnt >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else if (PREP && cnt == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (PREP && cnt == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    lds_barrier();
+  };
+  const unsigned xlane = (unsigned)(s * 32 + 8 * h) * 2u;
+  auto xload = [&](int64_t row0, f16x8 (&x)[KS0][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < KS0; ++ks) {
+      const int so = (int)((((unsigned)(ks >> 1) * (unsigned)a.x_mpad + (unsigned)row0) * 32u + 16u * (ks & 1)) * 2u);
+      x[ks][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rxh, xlane, so, 0));
+      x[ks][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rxl, xlane, so, 0));
+    }
+  };
+  const unsigned hlane = (unsigned)(s * kRfLd + 4 * h) * 4u;   // H1 rows: lane part of the offset
+
+  f16x8 xt[KS0][2];
+  xload((int64_t)blockIdx.x * kRfTile + wv * 32, xt);
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the first tile's X, where hipcc's bookkeeping sees it
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_one(0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dma_one(1, 1, i);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_one(2, 2, i);
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == (int64_t)blockIdx.x;
+    const int64_t r0 = tile * kRfTile + wv * 32;
+    const int64_t r0n = r0 + (int64_t)gridDim.x * kRfTile;
+    const int rows = rows_of(r0);
+    f32x16 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = f32x16{};
+#pragma unroll 1
+    for (int tq = 0; tq < 2; ++tq) {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int t = 4 * tq + tt;
+        const int cA = 2 * t, sA = (2 * tt) % 4, cB = cA + 1, sB = (2 * tt + 1) % 4;
+        // ---- phase A: Z0^T slice t; chunk cA + 3 (a B chunk) DMA'd one piece per k-step ----
+        arrive(!first && t <= 1 ? 63 : (first && t == 0 ? 12 : 12 + S));
+        const int cA3 = cA + 3 < kFwChunks ? cA + 3 : cA + 3 - kFwChunks;
+        const cu32x4* SA = slot(sA);
+        f32x16 accA = f32x16{};
+        f16x8 fa[2][2];
+        auto lda = [&](int ks, f16x8 (&f)[2]) __attribute__((always_inline)) {
+          const int au = s * 16 + ((2 * ks + h) ^ (s & 15));
+          f[0] = __builtin_bit_cast(f16x8, SA[au]);
+          f[1] = __builtin_bit_cast(f16x8, SA[512 + au]);
+        };
+        lda(0, fa[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS0; ++ks) {
+          __builtin_amdgcn_sched_barrier(0);
+          dma_one(cA3, (sA + 3) % 4, ks);
+          if (ks + 1 < KS0) lda(ks + 1, fa[(ks + 1) & 1]);
+          accA = rf_mfma3(fa[ks & 1][0], fa[ks & 1][1], xt[ks][0], xt[ks][1], accA);
+          if (RF_SGB && ks + 1 < KS0) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- epilogue: H1 slice t (lane: state s, features 8 (r >> 2) + 4 h + (r & 3)), the phase-B A operand ----
+        float hv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          hv[r] = tanh_fast(accA[r] * uA + cvec[0][32 * t + 8 * (r >> 2) + 4 * h + (r & 3)]);
+        if constexpr (PREP) {
+          const __amdgpu_buffer_rsrc_t rh1 =
+              __builtin_amdgcn_make_buffer_rsrc((void*)(a.H1 + r0 * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(cu32x4, f32x4{hv[4 * j], hv[4 * j + 1], hv[4 * j + 2], hv[4 * j + 3]}), rh1,
+                hlane, (32 * t + 8 * j) * 4, 0);
+        }
+        f16x8 aH[2][2];
+#pragma unroll
+        for (int uu = 0; uu < 2; ++uu) rf_split8(hv + 8 * uu, sH, aH[uu][0], aH[uu][1]);
+        // ---- phase B: Z1 += H1_t W1_t, all 256 columns; chunk cB + 3 (an A chunk) DMA'd over the first 4 steps ----
+        arrive(!first && t == 0 ? 63 : (first && t == 0 ? 12 + S : 12 + 2 * S));
+        const int cB3 = cB + 3 < kFwChunks ? cB + 3 : cB + 3 - kFwChunks;
+        const cu32x4* B = slot(sB);
+        f16x8 fb[2][2];
+        auto ldb = [&](int k, f16x8 (&f)[2]) __attribute__((always_inline)) {   // k = 8 nh + 4 uu + tn
+          const int col = 128 * (k >> 3) + 32 * (k & 3) + s;
+          const int bu = col * 4 + ((2 * ((k >> 2) & 1) + h) ^ ((col >> 2) & 3));
+          f[0] = __builtin_bit_cast(f16x8, B[bu]);
+          f[1] = __builtin_bit_cast(f16x8, B[1024 + bu]);
+        };
+        ldb(0, fb[0]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (k < 4) dma_one(cB3, (sB + 3) % 4, k);
+          if (k + 1 < 16) ldb(k + 1, fb[(k + 1) & 1]);
+          const int uu = (k >> 2) & 1, tn = k & 3, nh = k >> 3;
+          acc[4 * nh + tn] = rf_mfma3(aH[uu][0], aH[uu][1], fb[k & 1][0], fb[k & 1][1], acc[4 * nh + tn]);
+          if (RF_SGB && k + 1 < 16) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    xload(r0n < a.x_mpad ? r0n : 0, xt);   // the next tile's X, ahead of the H2 stores (see rfwd01_kernel)
+    // ---- H2 = tanh(acc 2^-P + b1): lane (column 32 tn + s, states 8 j + 4 h + i) ----
+    const __amdgpu_buffer_rsrc_t rz =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.H2 + r0 * kRfLd), 0, rows * kRfLd * 4, 0x00020000);
+    const unsigned zlane = (unsigned)(4 * h * kRfLd + s) * 4u;
+#pragma unroll
+    for (int tn = 0; tn < 8; ++tn) {
+      const float bn = cvec[1][32 * tn + s];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, tanh_fast(acc[tn][r] * uP + bn)), rz,
+                                              zlane, ((8 * (r >> 2) + (r & 3)) * kRfLd + 32 * tn) * 4, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup has left the CU
+}
+
 }  // namespace
 
 bool rfwd01_eligible(int L, const int* w, const int* wp) {
@@ -508,6 +720,27 @@ void launch_rfwd01(const Rfwd01Args& a, int num_cus, hipStream_t s) {
   const int64_t ntiles = (a.n + kRfTile - 1) / kRfTile;
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)num_cus);
   hipLaunchKernelGGL(rfwd01_kernel<8>, dim3(grid), dim3(kRfWaves * 64), 0, s, a);
+}
+
+bool fwd01_eligible(int L, const int* w, const int* wp) { return rfwd01_eligible(L, w, wp); }
+
+size_t fwd01_img_bytes() { return (size_t)kFwChunks * kRfUnits * 16; }
+
+void launch_fwd01_img(const float* th, int64_t offW0, int64_t offW1, int obs, const unsigned* am_w0,
+                      const unsigned* am_w1, uint16_t* img, hipStream_t s) {
+  hipLaunchKernelGGL(fwd01_img_kernel, dim3(8 * 1536 / 256), dim3(256), 0, s, th, offW0, offW1, obs, am_w0, am_w1,
+                     img);
+}
+
+void launch_fwd01(const Fwd01Args& a, int num_cus, hipStream_t s) {
+  if (a.n <= 0) return;
+  if (a.obs < 1 || a.obs > 128) throw std::runtime_error("fwd01: unsupported shape");
+  if ((int64_t)4 * a.x_mpad * 64 >= ((int64_t)1 << 31) || a.x_mpad < (a.n + kRfTile - 1) / kRfTile * kRfTile)
+    throw std::runtime_error("fwd01: X plane geometry");
+  const int64_t ntiles = (a.n + kRfTile - 1) / kRfTile;
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)num_cus);
+  if (a.H1) hipLaunchKernelGGL((fwd01_kernel<8, true>), dim3(grid), dim3(kRfWaves * 64), 0, s, a);
+  else hipLaunchKernelGGL((fwd01_kernel<8, false>), dim3(grid), dim3(kRfWaves * 64), 0, s, a);
 }
 
 }  // namespace trpo
