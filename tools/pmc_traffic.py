@@ -28,8 +28,9 @@ SPECS = {
     "fvp_rfwd01": ("rfwd01_kernel<8>", 1, 0),                               # layers 0 + 1 R-forward (rfwd.hip)
     "fvp_rbwdwg_l1": ("rbwd0_kernel<2>", 1, 0),                             # R-backward + X^T RD_0 (rbwd0.hip)
     "fvp_tail_l2": ("fvp_tail_kernel", 1, 0),
-    # C2 / C3: the one-launch FVP (fused16.hip mode 0; every substring must be in the name)
-    "fvp_fused": (("fvp_fused16_kernel<", ", 0>("), 1, 0),
+    # C2 / C3: the one-launch FVP (fused16.hip <FW, LB, TI0, OTA, MODE, NH> with MODE 0, the only zero argument;
+    # every substring must be in the name)
+    "fvp_fused": (("fvp_fused16_kernel<", ", 0, "), 1, 0),
 }
 # tags whose kernel is shared with a 1-segment policy-gradient launch: keep the long ones
 LONGEST = {
