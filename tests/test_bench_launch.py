@@ -183,3 +183,20 @@ def test_fused_fvp_roofline_follows_the_issued_arithmetic():
     assert bench.tag_bytes("ls_fwd", c3, n) == 4.0 * n * (128 + 18)
     assert bench.tag_bytes("fwd", c3, n) == 4.0 * n * (128 + 4 * 18 + 64 + 64)
     assert bench.tag_flops("ls_fwd_l1", c3, n) == 2.0 * n * 64 * 64
+
+
+def test_rfwd_tags_price_layers_0_and_1_together():
+    """rfwd.hip's one-launch tags at C4 widths: fvp_rfwd01 (X V0 + RH1 W1 + H1 V1; X planes, H1 in, RH1 and RZ2 out)
+    and the forwards' fwd_l01 / ls_fwd_l01 (X W0 + H1 W1; H1 out only in the prepare pass), all on the 3-product
+    f16 split and reading X -- not the per-layer pricing their "_l01" suffix would otherwise select."""
+    c4 = [128, 256, 256, 18]
+    n = 1000
+    assert bench.tag_flops("fvp_rfwd01", c4, n) == 2.0 * n * 128 * 256 + 4.0 * n * 256 * 256
+    assert bench.tag_bytes("fvp_rfwd01", c4, n) == 4.0 * n * (128 + 2 * 256 + 256)
+    for tag in ("fwd_l01", "ls_fwd_l01"):
+        assert bench.tag_flops(tag, c4, n) == 2.0 * n * (128 * 256 + 256 * 256)
+        assert bench.tag_is_split(tag, c4) and bench.tag_products(tag, c4) == 3
+        assert bench.tag_x_bytes(tag, c4, n) == 4.0 * n * 128
+    assert bench.tag_bytes("fwd_l01", c4, n) == 4.0 * n * (128 + 256 + 256)
+    assert bench.tag_bytes("ls_fwd_l01", c4, n) == 4.0 * n * (128 + 256)
+    assert bench.tag_products("fvp_rfwd01", c4) == 3 and bench.tag_x_bytes("fvp_rfwd01", c4, n) == 4.0 * n * 128
